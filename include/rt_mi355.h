@@ -1,0 +1,239 @@
+/*
+ * rt_mi355.h — C-ABI of the MI355X (gfx950) trace path.
+ *
+ * This is the drop-in boundary for the per-pixel trace loop of
+ * vectorized-runner/unity-raytracer (reference @ v1).  The reference has no
+ * native code and no `Render(Scene, Camera)` method; its frame-level seam is
+ *
+ *     RayTracingSetup.CastPixelRays(CameraData)
+ *         Assets/RayTracer/Demo-RayTracing/RayTracingSetup.cs:275-302
+ *
+ * which reads the implicit inputs `Scene` (Data/Objects/Scene.cs:8-15),
+ * `ImagePlane` (:21), `BackgroundColor` (:22), `MaxReflectionBounces` (:23)
+ * and writes `Color[] PixelColors` (:40).  The entry points below replace
+ * that method (and, for batch ray queries, `Scene.IntersectRay`,
+ * Data/Objects/Scene.cs:43-122).  A Unity C# host binds them with
+ * [DllImport]; the stub is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Plain C types only; every struct is blittable (C# bool → int32).
+ *   - Every call returns 0 (RT_OK) or a negative rt_status; the message of
+ *     the last failure is available from rt_last_error().  No C++ exception
+ *     crosses this boundary.
+ *   - Calls on one context are synchronous and not thread-safe (the
+ *     reference calls CastPixelRays once per frame from Update() on Unity's
+ *     main thread, RayTracingSetup.cs:171-199).
+ *   - The caller owns every input array and output buffer; the library
+ *     copies what it needs and retains no caller pointer.
+ *   - All arithmetic is IEEE float32 with the operation order of the
+ *     reference (see DESIGN.md "Arithmetic contract").
+ */
+#ifndef RT_MI355_H
+#define RT_MI355_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_E_INVALID = -1,   /* bad argument (null pointer, negative size, spp not n*n ...)   */
+    RT_E_SCENE = -2,     /* malformed scene (index out of range, mesh range overflow ...) */
+    RT_E_HIP = -3,       /* a HIP runtime call failed (message carries hipGetErrorString) */
+    RT_E_NO_DEVICE = -4, /* no gfx950 device visible                                      */
+    RT_E_STATE = -5,     /* call order (e.g. rt_render before rt_set_scene)                */
+    RT_E_INTERNAL = -6   /* internal invariant broken; reference analog: the
+                            ArgumentOutOfRangeException of a None hit type,
+                            RayTracingSetup.cs:432-434                              */
+} rt_status;
+
+/* ---- POD types mirroring the reference's structs ----------------------- */
+
+/* Unity.Mathematics.float3 */
+typedef struct rt_float3 { float x, y, z; } rt_float3;
+
+/* Triangle, Data/Objects/Triangle.cs:7-11 (36 B) */
+typedef struct rt_triangle { rt_float3 vertex0, vertex1, vertex2; } rt_triangle;
+
+/* Sphere, Data/Objects/Sphere.cs:7-10 (16 B) — stores the SQUARED radius */
+typedef struct rt_sphere { rt_float3 center; float radius_squared; } rt_sphere;
+
+/* AABB, Data/Collision/AABB.cs:5-8 (24 B) */
+typedef struct rt_aabb { rt_float3 min, max; } rt_aabb;
+
+/* MaterialData, Data/Shading/MaterialData.cs:7-15 (56 B; C# bool → int32) */
+typedef struct rt_material {
+    rt_float3 diffuse_reflectance;
+    rt_float3 ambient_reflectance;
+    rt_float3 mirror_reflectance;
+    rt_float3 specular_reflectance;
+    float phong_exponent;
+    int32_t is_mirror;
+} rt_material;
+
+/* PointLightData, Data/Lights/PointLightData.cs:7-11 (24 B) */
+typedef struct rt_point_light { rt_float3 position, intensity; } rt_point_light;
+
+/* CameraData, Data/Camera/CameraData.cs:5-11 (48 B).  Forward/Right/Up are
+ * the already-normalised basis built in RayTracingSetup.Update() :175-181. */
+typedef struct rt_camera { rt_float3 position, forward, right, up; } rt_camera;
+
+/* ImagePlane, Data/Camera/ImagePlane.cs:11-45 (Resolution inlined, 20 B) */
+typedef struct rt_image_plane {
+    int32_t resolution_x, resolution_y;
+    float distance_to_camera;
+    float half_horizontal_length;
+    float half_vertical_length;
+} rt_image_plane;
+
+/* Mesh, Data/Objects/Mesh.cs:7-13, flattened: its Triangles[] and
+ * TriangleNormals[] are the range [first_triangle, first_triangle +
+ * triangle_count) of rt_scene_desc.mesh_triangles / mesh_triangle_normals. */
+typedef struct rt_mesh {
+    int32_t first_triangle;
+    int32_t triangle_count;
+    rt_material material;
+    rt_aabb aabb;   /* Mesh.AABB over ALL transformed vertices, SceneMesh.cs:22-31 */
+} rt_mesh;
+
+/* Scene, Data/Objects/Scene.cs:8-15.  Order inside every array is the order
+ * of the reference's List<>s and fixes the closest-hit tie winner
+ * (meshes by index then triangle index, then spheres, then loose
+ * triangles; first wins, Scene.cs:75,93,108). */
+typedef struct rt_scene_desc {
+    /* TriangleData, Data/Objects/TriangleData.cs:8-13 */
+    const rt_triangle *triangles;
+    const rt_float3 *triangle_normals;      /* Triangle.Normal, Triangle.cs:13-21   */
+    const rt_material *triangle_materials;
+    int32_t triangle_count;
+    /* MeshData, Data/Objects/MeshData.cs:7-9 */
+    const rt_triangle *mesh_triangles;
+    const rt_float3 *mesh_triangle_normals; /* -Triangle.Normal, SceneMesh.cs:43    */
+    int32_t mesh_triangle_total;
+    const rt_mesh *meshes;
+    int32_t mesh_count;
+    /* SphereData, Data/Objects/SphereData.cs:7-10 */
+    const rt_sphere *spheres;
+    const rt_material *sphere_materials;
+    int32_t sphere_count;
+    /* PointLights / AmbientLight, Scene.cs:12-13 */
+    const rt_point_light *point_lights;
+    int32_t point_light_count;
+    rt_float3 ambient_radiance;             /* AmbientLightData.Radiance            */
+} rt_scene_desc;
+
+/* Frame parameters: the serialized fields of RayTracingSetup (:22-23) plus
+ * the build's documented extensions (DESIGN.md "Extensions"). */
+typedef struct rt_render_params {
+    float background_color[4];      /* UnityEngine.Color (0..1); alpha ignored, Rgb.cs:15-18 */
+    int32_t max_reflection_bounces; /* MaxReflectionBounces (:23)                  */
+    int32_t samples_per_pixel;      /* n*n stratified samples; 1 == reference        */
+    int32_t band_index;             /* block-cyclic row sharding: this shard          */
+    int32_t band_count;             /*   number of shards (1 = whole image)           */
+    int32_t band_rows;              /*   rows per block (0 → 8)                       */
+    int32_t flags;                  /* RT_FLAG_*                                      */
+} rt_render_params;
+
+#define RT_FLAG_COUNT_TESTS 1   /* fill rt_stats box/triangle/sphere counters (slower) */
+
+/* Work counters and timings of the last render. */
+typedef struct rt_stats {
+    uint64_t primary_rays;     /* camera samples traced                          */
+    uint64_t shadow_rays;      /* one per (hit, point light), :327-333           */
+    uint64_t reflection_rays;  /* mirror bounces, :358-363                        */
+    uint64_t box_tests;        /* BVH node/AABB slab tests   (RT_FLAG_COUNT_TESTS) */
+    uint64_t triangle_tests;   /* Möller–Trumbore tests      (RT_FLAG_COUNT_TESTS) */
+    uint64_t sphere_tests;     /* ray/sphere tests           (RT_FLAG_COUNT_TESTS) */
+    uint64_t shading_fetches;  /* closest hits shaded (normal + material fetch)    */
+    double kernel_ms;          /* device time of the trace kernel(s)              */
+    double total_ms;           /* wall time of the whole call                     */
+} rt_stats;
+
+/* Closest-hit record, IntersectionResult (Data/Collision/IntersectionResult.cs:3-7)
+ * with ObjectId (Data/Objects/ObjectId.cs:5-9) inlined.  type: 0 None,
+ * 1 Sphere, 2 Triangle, 3 MeshTriangle (ObjectType.cs:3-9). */
+typedef struct rt_hit {
+    int32_t type;
+    int32_t index;
+    int32_t mesh_index;
+    float distance;
+} rt_hit;
+
+/* Ray, Data/Collision/Ray.cs:7-10 (24 B) */
+typedef struct rt_ray { rt_float3 origin, direction; } rt_ray;
+
+/* ---- entry points ------------------------------------------------------- */
+
+typedef struct rt_ctx rt_ctx;
+
+/* ABI version of the loaded library (== RT_ABI_VERSION it was built with). */
+int32_t rt_abi_version(void);
+
+/* Create a context on the calling thread's current HIP device.  num_gpus
+ * must be 1 (one context per GPU; multi-GPU frames shard rows with
+ * rt_render_params.band_index/band_count across one process per GPU). */
+int rt_create(rt_ctx **out_ctx, int32_t num_gpus);
+
+/* Destroy a context (null is a no-op). */
+void rt_destroy(rt_ctx *ctx);
+
+/* Message of the last failed call on ctx (or of the last failed rt_create
+ * when ctx is null).  Never null; valid until the next call on ctx. */
+const char *rt_last_error(const rt_ctx *ctx);
+
+/* Use this HIP stream (hipStream_t passed as void*) for all device work;
+ * null selects the context's own stream. */
+int rt_set_stream(rt_ctx *ctx, void *hip_stream);
+
+/* Upload a scene: copies every array to HBM, computes Scene.AABB exactly as
+ * Scene.CalculateAABB (Scene.cs:17-41) and builds the BVH.  Replaces
+ * RayTracingSetup.UpdateScene()'s result (:120-128). */
+int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *scene);
+
+/* Render one frame: the MI355X replacement of CastPixelRays (:275-302).
+ * out_rgba is a caller-owned HOST buffer of resolution_x*resolution_y*4
+ * floats (row-major, y = 0 is the top row, alpha = 1), i.e. PixelColors.
+ * When band_count > 1, only this shard's rows are rendered and out_rgba
+ * receives the shard's compact buffer (rt_band_rows_local rows). */
+int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
+              const rt_render_params *params, float *out_rgba, rt_stats *stats);
+
+/* Same as rt_render but the output stays in HBM: d_out_rgba is a DEVICE
+ * pointer on the context's GPU of at least out_bytes bytes.  The call
+ * returns after the frame is complete on the device. */
+int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
+                     const rt_render_params *params, float *d_out_rgba, size_t out_bytes,
+                     rt_stats *stats);
+
+/* Rows of the compact per-shard buffer for (resolution_y, band_index,
+ * band_count, band_rows). */
+int32_t rt_band_rows_local(int32_t resolution_y, int32_t band_index, int32_t band_count,
+                           int32_t band_rows);
+
+/* Reassemble an image from band_count gathered shard buffers laid out
+ * back to back (each rt_band_rows_local(max) rows, padded) into row order.
+ * Both pointers are DEVICE pointers on the context's GPU. */
+int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x,
+                      int32_t resolution_y, int32_t band_count, int32_t band_rows,
+                      float *d_image);
+
+/* Batch closest-hit query: Scene.IntersectRay (Scene.cs:43-122) for n host
+ * rays; writes n host rt_hit records. */
+int rt_intersect_rays(rt_ctx *ctx, const rt_ray *rays, int32_t n, rt_hit *out_hits);
+
+/* Diagnostic: the float threshold T with  d < T  <=>  degrees(acos(d)) > 90f
+ * (RayTracingSetup.cs:384-392), which the kernels use instead of acos so the
+ * discrete specular branch matches the host libm bit for bit. */
+float rt_spec_threshold(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_MI355_H */

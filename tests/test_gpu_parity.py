@@ -1,0 +1,167 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bar: max |gpu - oracle| <= 1e-4 per RGB channel in Color units (north_star);
+the arithmetic is the reference's float32 op order on both sides, so the
+observed error is normally exactly 0.  Ray counts (primary / shadow /
+reflection) must match the oracle exactly — they are integer decisions.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4  # per RGB channel, Color units (Rgb.Color = Value / 255)
+
+
+def _render(ctx, rt, fr, **kw):
+    ctx.set_scene(fr.scene)
+    img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
+    return img, st
+
+
+def _check(img, ref, st, counts, name):
+    assert img.shape == ref.shape
+    err = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    assert np.isfinite(img).all() == np.isfinite(ref).all()
+    mx = float(np.nanmax(err)) if err.size else 0.0
+    assert mx <= TOL, f"{name}: max err {mx} at {np.unravel_index(np.nanargmax(err), err.shape)}"
+    got = (st.primary_rays, st.shadow_rays, st.reflection_rays)
+    want = (counts["primary_rays"], counts["shadow_rays"], counts["reflection_rays"])
+    assert got == want, f"{name}: ray counts {got} != oracle {want}"
+
+
+@pytest.mark.parametrize("name,res,spp", [
+    ("demo", None, 1),
+    ("C1", None, 1),
+    ("C2", (192, 108), 4),
+    ("C2", (64, 36), 9),
+    ("C3", (96, 54), 4),
+    ("C5", (48, 27), 4),
+])
+def test_frame_vs_oracle(gpu_ctx, rt, orc, name, res, spp):
+    fr = rt.make(name)
+    if res:
+        fr = fr.with_resolution(*res)
+    fr = fr.with_(spp=spp)
+    img, st = _render(gpu_ctx, rt, fr)
+    ref, counts = orc.render(fr)
+    _check(img, ref, st, counts, name)
+
+
+def test_goldens(gpu_ctx, rt):
+    """Committed fixtures (tests/golden/, made by tests/golden/make_golden.py)."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "frames.npz"))
+    for name in ("demo", "C1"):
+        fr = rt.make(name)
+        img, st = _render(gpu_ctx, rt, fr)
+        ref = g[name]
+        assert float(np.max(np.abs(img[..., :3] - ref))) <= TOL
+        assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == tuple(g[name + "_counts"])
+
+
+def test_full_size_c3_sampled_pixels(gpu_ctx, rt, orc):
+    """BASELINE config C3 at full size (1920x1080, 4 spp, depth 8): the GPU
+    frame against the oracle on 400 seeded pixels (pixels are independent,
+    RayTracingSetup.cs:288-301)."""
+    fr = rt.make("C3")
+    img, st = _render(gpu_ctx, rt, fr)
+    rng = np.random.default_rng(7)
+    idx = rng.choice(fr.plane.ResolutionX * fr.plane.ResolutionY, 400, replace=False).astype(np.int32)
+    ref, _ = orc.render_pixels(fr, idx)
+    got = img.reshape(-1, 4)[idx]
+    assert float(np.max(np.abs(got - ref))) <= TOL
+    assert st.primary_rays == 1920 * 1080 * 4
+
+
+def test_intersect_rays_exact(gpu_ctx, rt, orc):
+    """Scene.IntersectRay batch query: type, index, mesh index and distance
+    equal the brute-force oracle exactly, incl. rays leaving surfaces."""
+    for name in ("demo", "C2", "C3", "C5"):
+        fr = rt.make(name)
+        gpu_ctx.set_scene(fr.scene)
+        rng = np.random.default_rng(11)
+        n = 4000 if name != "C5" else 1500
+        o = rng.uniform(-1.2, 1.2, (n, 3)).astype(np.float32)
+        if name == "demo":
+            o *= 30
+        d = rng.normal(size=(n, 3)).astype(np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        d[: n // 10, 0] = 0.0  # axis-parallel components (rcp = +-inf)
+        rays = np.concatenate([o, d.astype(np.float32)], 1)
+        hits = gpu_ctx.intersect_rays(rays)
+        ref = orc.intersect(fr.scene, rays)
+        for f in ("type", "index", "mesh_index"):
+            assert np.array_equal(hits[f], ref[f]), (name, f)
+        assert np.array_equal(hits["distance"].view(np.uint32), ref["distance"].view(np.uint32)), name
+
+
+def test_determinism_and_bands(gpu_ctx, rt):
+    """Two renders are bit-identical; row shards reassembled equal the full frame."""
+    import torch
+    fr = rt.make("C2").with_resolution(200, 123)
+    a, _ = _render(gpu_ctx, rt, fr)
+    b, _ = _render(gpu_ctx, rt, fr)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for bands in (2, 3, 8):
+        rows = gpu_ctx.lib.rt_band_rows_local(fr.plane.ResolutionY, 0, bands, 8)
+        parts = []
+        for k in range(bands):
+            img, _ = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, band_index=k, band_count=bands))
+            assert img.shape[0] == rows
+            parts.append(img)
+        gathered = torch.from_numpy(np.stack(parts)).cuda()
+        full = torch.empty((fr.plane.ResolutionY, fr.plane.ResolutionX, 4), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.assemble_bands(gathered.data_ptr(), fr.plane.ResolutionX, fr.plane.ResolutionY, bands, 8,
+                               full.data_ptr())
+        assert np.array_equal(full.cpu().numpy().view(np.uint32), a.view(np.uint32)), bands
+
+
+def test_edge_cases(gpu_ctx, rt, orc):
+    S = rt.Scene
+    fr0 = rt.make("C1").with_resolution(32, 24)
+    # empty scene: everything is background (Shade :310-311)
+    empty = fr0.with_(scene=S(), background=(0.25, 0.5, 1.0, 1.0))
+    img, st = _render(gpu_ctx, rt, empty)
+    assert np.allclose(img[..., :3], np.array([0.25, 0.5, 1.0], np.float32) * np.float32(255) / np.float32(255))
+    assert st.shadow_rays == 0
+    # spheres only / loose triangles only / one mesh only
+    c1 = fr0.scene
+    only_sph = S()
+    only_sph.SphereData = c1.SphereData
+    only_sph.PointLights = c1.PointLights
+    only_sph.AmbientLight = c1.AmbientLight
+    only_tri = S()
+    only_tri.TriangleData = c1.TriangleData
+    only_tri.PointLights = c1.PointLights
+    for sc in (only_sph, only_tri):
+        f = fr0.with_(scene=sc)
+        img, st = _render(gpu_ctx, rt, f)
+        ref, counts = orc.render(f)
+        _check(img, ref, st, counts, "edge")
+    # no lights, negative / zero bounces, zero resolution
+    for kw in (dict(max_bounces=0), dict(max_bounces=-1)):
+        f = fr0.with_(**kw)
+        img, st = _render(gpu_ctx, rt, f)
+        ref, counts = orc.render(f)
+        _check(img, ref, st, counts, "bounces")
+    f = fr0.with_resolution(0, 0)
+    img, st = _render(gpu_ctx, rt, f)
+    assert img.size == 0 and st.primary_rays == 0
+
+
+def test_errors(gpu_ctx, rt):
+    fr = rt.make("C1").with_resolution(8, 8)
+    gpu_ctx.set_scene(fr.scene)
+    with pytest.raises(rt.RtError) as e:
+        gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, spp=2))
+    assert e.value.status == rt.abi.RT_E_INVALID
+    with pytest.raises(rt.RtError) as e:
+        gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, band_index=3, band_count=2))
+    assert e.value.status == rt.abi.RT_E_INVALID
+    fresh = rt.Context()
+    with pytest.raises(rt.RtError) as e:
+        fresh.render(fr.camera, fr.plane, rt.frame_params(fr))
+    assert e.value.status == rt.abi.RT_E_STATE
+    fresh.close()

@@ -1,0 +1,23 @@
+// kernels.h — host-side launchers of the gfx950 kernels in trace.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_device.h"
+
+namespace rtk {
+
+// One frame (or one row shard of it): CastPixelRays + Shade, RayTracingSetup.cs:275-366.
+hipError_t launch_render(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
+                         hipStream_t stream);
+
+// Batch closest hit, Scene.IntersectRay (Scene.cs:43-122): rays are 6 floats
+// (origin, direction); out[i] = {rank or -1, distance bits, -, -}.
+hipError_t launch_intersect(const rtd::SceneDev &S, const float *rays, int n, int4 *out,
+                            hipStream_t stream);
+
+// Row-order reassembly of block-cyclic shards gathered back to back.
+hipError_t launch_assemble(const float4 *gathered, int res_x, int res_y, int band_count,
+                           int band_rows, int local_rows, float4 *image, hipStream_t stream);
+
+}  // namespace rtk

@@ -1,0 +1,628 @@
+// rt_abi.cpp — implementation of the C-ABI in include/rt_mi355.h.
+//
+// Host side of the MI355X trace path: validates the reference-shaped scene,
+// computes Scene.CalculateAABB exactly (Scene.cs:17-41), builds the BVH,
+// lays the scene out in HBM (rt_device.h) and launches the gfx950 kernels
+// (trace.hip).  There is no CPU fallback: without a gfx950 device every
+// entry point fails with RT_E_NO_DEVICE / RT_E_HIP.
+#include "../../include/rt_mi355.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "bvh.h"
+#include "kernels.h"
+#include "rt_device.h"
+#include "rt_math.h"
+
+namespace {
+
+struct DeviceArrays {
+    void *nodes = nullptr, *leaves = nullptr, *tris = nullptr, *sphs = nullptr, *shade = nullptr,
+         *mats = nullptr, *lights = nullptr, *gates = nullptr;
+};
+
+}  // namespace
+
+struct rt_ctx {
+    int device = -1;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    bool has_scene = false;
+    DeviceArrays arr;
+    rtd::SceneDev S{};
+    std::vector<int> mesh_rank_first;  // prefix of mesh triangle counts (rank decode)
+    int mesh_tri_ranks = 0, sphere_count = 0, loose_count = 0;
+    float4 *d_out = nullptr;
+    size_t d_out_cap = 0;
+    unsigned long long *d_counters = nullptr;
+    float *d_rays = nullptr;
+    int4 *d_hits = nullptr;
+    size_t rays_cap = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_build_ms = 0.0;
+    int last_bvh_depth = 0;
+};
+
+namespace {
+
+thread_local std::string g_create_error;
+
+int fail(rt_ctx *ctx, int status, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx)
+        ctx->err = buf;
+    else
+        g_create_error = buf;
+    return status;
+}
+
+#define HIP_OR_FAIL(ctx, call)                                                                   \
+    do {                                                                                         \
+        hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail((ctx), RT_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_));         \
+    } while (0)
+
+void free_scene(rt_ctx *c) {
+    void **ps[] = {&c->arr.nodes, &c->arr.leaves, &c->arr.tris, &c->arr.sphs,
+                   &c->arr.shade, &c->arr.mats,   &c->arr.lights, &c->arr.gates};
+    for (void **p : ps) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+    c->has_scene = false;
+}
+
+template <typename T>
+hipError_t upload(void **dst, const std::vector<T> &v) {
+    if (v.empty()) return hipSuccess;
+    hipError_t e = hipMalloc(dst, v.size() * sizeof(T));
+    if (e != hipSuccess) return e;
+    return hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+rtm::f3 F3(const rt_float3 &v) { return rtm::mk(v.x, v.y, v.z); }
+
+// Ordered-integer view of a float for bisection over representable values.
+int32_t fkey(float f) {
+    uint32_t b;
+    std::memcpy(&b, &f, 4);
+    return (b & 0x80000000u) ? -(int32_t)(b & 0x7fffffffu) : (int32_t)b;
+}
+float ffrom(int32_t k) {
+    uint32_t b = k < 0 ? (0x80000000u | (uint32_t)(-k)) : (uint32_t)k;
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+}
+
+// The reference's specular back-face test (RayTracingSetup.cs:382-392):
+//   degrees(acos(d)) > 90f,  acos = (float)System.Math.Acos((double)d),
+//   degrees(x) = x * 57.29578f.
+// It is monotone non-increasing in d, so it equals d < T for the smallest
+// float T where it is false.  T is found here once with the host libm (the
+// same double acos the CPU oracle uses) so the GPU never evaluates acos.
+bool spec_backfacing(float d) { return (float)std::acos((double)d) * 57.29578f > 90.0f; }
+
+float compute_spec_threshold() {
+    int32_t lo = fkey(-1.0f), hi = fkey(1.0f);  // backfacing(lo) true, backfacing(hi) false
+    while (hi - lo > 1) {
+        int32_t mid = lo + (hi - lo) / 2;
+        if (spec_backfacing(ffrom(mid)))
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return ffrom(hi);
+}
+
+float spec_threshold() {
+    static const float T = compute_spec_threshold();
+    return T;
+}
+
+bool mat_less(const rt_material &a, const rt_material &b) { return std::memcmp(&a, &b, sizeof a) < 0; }
+
+rtd::DevMaterial to_dev(const rt_material &m) {
+    rtd::DevMaterial d;
+    d.kd_phong = make_float4(m.diffuse_reflectance.x, m.diffuse_reflectance.y, m.diffuse_reflectance.z,
+                             m.phong_exponent);
+    d.ka_mirror = make_float4(m.ambient_reflectance.x, m.ambient_reflectance.y, m.ambient_reflectance.z,
+                              m.is_mirror ? 1.0f : 0.0f);
+    d.km = make_float4(m.mirror_reflectance.x, m.mirror_reflectance.y, m.mirror_reflectance.z, 0.0f);
+    d.ks = make_float4(m.specular_reflectance.x, m.specular_reflectance.y, m.specular_reflectance.z, 0.0f);
+    return d;
+}
+
+int isqrt_exact(int v) {
+    if (v <= 0) return -1;
+    int n = 1;
+    while (n * n < v) ++n;
+    return n * n == v ? n : -1;
+}
+
+int32_t band_local_rows(int32_t res_y, int32_t band_count, int32_t band_rows) {
+    if (res_y <= 0) return 0;
+    if (band_count <= 1) return res_y;
+    const int32_t blocks = (res_y + band_rows - 1) / band_rows;
+    const int32_t slots = (blocks + band_count - 1) / band_count;
+    return slots * band_rows;
+}
+
+int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, const rt_render_params *prm,
+                  rtd::FrameDev &F, size_t &out_bytes) {
+    if (!cam || !plane || !prm) return fail(ctx, RT_E_INVALID, "null camera/plane/params");
+    if (!ctx->has_scene) return fail(ctx, RT_E_STATE, "rt_render before rt_set_scene");
+    if (plane->resolution_x < 0 || plane->resolution_y < 0)
+        return fail(ctx, RT_E_INVALID, "negative resolution (%d, %d)", plane->resolution_x, plane->resolution_y);
+    const int n = isqrt_exact(prm->samples_per_pixel);
+    if (n < 0 || n > 8)
+        return fail(ctx, RT_E_INVALID, "samples_per_pixel must be n*n with 1 <= n <= 8, got %d",
+                    prm->samples_per_pixel);
+    if (prm->max_reflection_bounces > rtd::kMaxBounces)
+        return fail(ctx, RT_E_INVALID, "max_reflection_bounces %d > %d unsupported", prm->max_reflection_bounces,
+                    rtd::kMaxBounces);
+    const int band_count = prm->band_count <= 0 ? 1 : prm->band_count;
+    const int band_rows = prm->band_rows <= 0 ? 8 : prm->band_rows;
+    if (prm->band_index < 0 || prm->band_index >= band_count)
+        return fail(ctx, RT_E_INVALID, "band_index %d outside [0, %d)", prm->band_index, band_count);
+    std::memset(&F, 0, sizeof F);
+    // ImagePlane.GetRect(cameraData).TopLeft (ImagePlane.cs:26-44)
+    const rtm::f3 center = F3(cam->position) + F3(cam->forward) * plane->distance_to_camera;
+    const rtm::f3 half_up = F3(cam->up) * plane->half_vertical_length;
+    const rtm::f3 half_right = F3(cam->right) * plane->half_horizontal_length;
+    const rtm::f3 tl = (center - half_right) + half_up;
+    F.cam_pos[0] = cam->position.x; F.cam_pos[1] = cam->position.y; F.cam_pos[2] = cam->position.z;
+    F.right[0] = cam->right.x; F.right[1] = cam->right.y; F.right[2] = cam->right.z;
+    F.up[0] = cam->up.x; F.up[1] = cam->up.y; F.up[2] = cam->up.z;
+    F.top_left[0] = tl.x; F.top_left[1] = tl.y; F.top_left[2] = tl.z;
+    F.hl = plane->half_horizontal_length * 2.0f;  // HorizontalLength, ImagePlane.cs:23
+    F.vl = plane->half_vertical_length * 2.0f;
+    for (int i = 0; i < 3; ++i) F.bg255[i] = prm->background_color[i] * 255.0f;  // Rgb(Color), Rgb.cs:15-18
+    F.res_x = plane->resolution_x;
+    F.res_y = plane->resolution_y;
+    F.spp = n * n;
+    F.spp_n = n;
+    F.max_bounces = prm->max_reflection_bounces;
+    F.band_index = prm->band_index;
+    F.band_count = band_count;
+    F.band_rows = band_rows;
+    F.local_rows = band_local_rows(F.res_y, band_count, band_rows);
+    // tile: 64/spp pixels per wave, square when that is a power of four
+    const int ppw = rtd::kWaveSize / F.spp;
+    int tw = ppw, th = 1;
+    for (int s = 1; s * s <= ppw; ++s)
+        if (s * s == ppw) { tw = s; th = s; }
+    F.tile_w = tw;
+    F.tile_h = th;
+    F.tiles_x = (F.res_x + tw - 1) / tw;
+    const int tiles_y = (F.local_rows + th - 1) / th;
+    F.num_tiles = F.res_x > 0 ? F.tiles_x * tiles_y : 0;
+    out_bytes = (size_t)F.local_rows * F.res_x * sizeof(float4);
+    return RT_OK;
+}
+
+int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, float4 *d_out, rt_stats *stats,
+              std::chrono::steady_clock::time_point t_start, float *host_out, size_t out_bytes) {
+    F.out = d_out;
+    F.counters = ctx->d_counters;
+    HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_OR_FAIL(ctx, rtk::launch_render(ctx->S, F, (prm->flags & RT_FLAG_COUNT_TESTS) != 0, ctx->stream));
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    unsigned long long counts[8] = {0};
+    HIP_OR_FAIL(ctx, hipMemcpyAsync(counts, ctx->d_counters, sizeof counts, hipMemcpyDeviceToHost, ctx->stream));
+    if (host_out && out_bytes)
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    if (stats) {
+        float ms = 0.0f;
+        HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        stats->primary_rays = counts[0];
+        stats->shadow_rays = counts[1];
+        stats->reflection_rays = counts[2];
+        stats->box_tests = counts[3];
+        stats->triangle_tests = counts[4];
+        stats->sphere_tests = counts[5];
+        stats->shading_fetches = counts[6];
+        stats->kernel_ms = ms;
+        stats->total_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+float rt_spec_threshold(void) { return spec_threshold(); }
+
+int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
+    if (!out_ctx) return fail(nullptr, RT_E_INVALID, "out_ctx is null");
+    *out_ctx = nullptr;
+    if (num_gpus != 1)
+        return fail(nullptr, RT_E_INVALID,
+                    "num_gpus must be 1: one context per GPU; shard rows with band_index/band_count");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(nullptr, RT_E_NO_DEVICE, "no HIP device visible");
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(nullptr, RT_E_NO_DEVICE, "hipGetDevice failed");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return fail(nullptr, RT_E_NO_DEVICE, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, RT_E_NO_DEVICE, "device %d is %s; this library is built for gfx950 (MI355X)", dev,
+                    prop.gcnArchName);
+    rt_ctx *c = new rt_ctx();
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        rt_destroy(c);
+        return fail(nullptr, RT_E_HIP, "stream/event/counter allocation failed");
+    }
+    c->stream = c->own_stream;
+    *out_ctx = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_scene(ctx);
+    if (ctx->d_out) (void)hipFree(ctx->d_out);
+    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_rays) (void)hipFree(ctx->d_rays);
+    if (ctx->d_hits) (void)hipFree(ctx->d_hits);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+const char *rt_last_error(const rt_ctx *ctx) {
+    if (!ctx) return g_create_error.c_str();
+    return ctx->err.c_str();
+}
+
+int rt_set_stream(rt_ctx *ctx, void *hip_stream) {
+    if (!ctx) return RT_E_INVALID;
+    ctx->stream = hip_stream ? (hipStream_t)hip_stream : ctx->own_stream;
+    return RT_OK;
+}
+
+int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
+    if (!ctx) return RT_E_INVALID;
+    if (!sc) return fail(ctx, RT_E_INVALID, "scene is null");
+    if (sc->triangle_count < 0 || sc->mesh_triangle_total < 0 || sc->mesh_count < 0 || sc->sphere_count < 0 ||
+        sc->point_light_count < 0)
+        return fail(ctx, RT_E_INVALID, "negative count in scene");
+    if ((sc->triangle_count && (!sc->triangles || !sc->triangle_normals || !sc->triangle_materials)) ||
+        (sc->mesh_count && !sc->meshes) ||
+        (sc->mesh_triangle_total && (!sc->mesh_triangles || !sc->mesh_triangle_normals)) ||
+        (sc->sphere_count && (!sc->spheres || !sc->sphere_materials)) ||
+        (sc->point_light_count && !sc->point_lights))
+        return fail(ctx, RT_E_INVALID, "null array with a non-zero count");
+    int64_t mesh_ranks = 0;
+    for (int m = 0; m < sc->mesh_count; ++m) {
+        const rt_mesh &M = sc->meshes[m];
+        if (M.triangle_count < 0 || M.first_triangle < 0 ||
+            (int64_t)M.first_triangle + M.triangle_count > sc->mesh_triangle_total)
+            return fail(ctx, RT_E_SCENE, "mesh %d range [%d, +%d) outside mesh_triangle_total %d", m,
+                        M.first_triangle, M.triangle_count, sc->mesh_triangle_total);
+        mesh_ranks += M.triangle_count;
+    }
+    if (mesh_ranks + sc->sphere_count + sc->triangle_count > (int64_t)(1 << 30))
+        return fail(ctx, RT_E_SCENE, "too many primitives");
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    free_scene(ctx);
+
+    const int MT = (int)mesh_ranks, NS = sc->sphere_count, NL = sc->triangle_count;
+    const int P = MT + NS + NL;
+
+    // Scene.CalculateAABB (Scene.cs:17-41) with Unity min/max semantics.
+    rtm::f3 smin = rtm::mk(FLT_MAX, FLT_MAX, FLT_MAX), smax = rtm::mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+    auto enc_box = [&](rtm::f3 lo, rtm::f3 hi) {  // AABB.Encapsulate(AABB): min(Min, other.Min)
+        smin = rtm::mk(rtm::umin(smin.x, lo.x), rtm::umin(smin.y, lo.y), rtm::umin(smin.z, lo.z));
+        smax = rtm::mk(rtm::umax(smax.x, hi.x), rtm::umax(smax.y, hi.y), rtm::umax(smax.z, hi.z));
+    };
+    auto enc_pt = [&](rtm::f3 p) {  // AABB.Encapsulate(float3): min(point, Min)
+        smin = rtm::mk(rtm::umin(p.x, smin.x), rtm::umin(p.y, smin.y), rtm::umin(p.z, smin.z));
+        smax = rtm::mk(rtm::umax(p.x, smax.x), rtm::umax(p.y, smax.y), rtm::umax(p.z, smax.z));
+    };
+    for (int m = 0; m < sc->mesh_count; ++m) enc_box(F3(sc->meshes[m].aabb.min), F3(sc->meshes[m].aabb.max));
+    for (int i = 0; i < NL; ++i) {
+        enc_pt(F3(sc->triangles[i].vertex0));
+        enc_pt(F3(sc->triangles[i].vertex1));
+        enc_pt(F3(sc->triangles[i].vertex2));
+    }
+    for (int i = 0; i < NS; ++i) {  // Sphere.AABB, Sphere.cs:17-22
+        const rtm::f3 c = F3(sc->spheres[i].center);
+        const float r = sqrtf(sc->spheres[i].radius_squared);
+        enc_box(rtm::mk(c.x - r, c.y - r, c.z - r), rtm::mk(c.x + r, c.y + r, c.z + r));
+    }
+
+    // Materials, deduplicated.
+    std::map<rt_material, int, bool (*)(const rt_material &, const rt_material &)> mat_ids(mat_less);
+    std::vector<rtd::DevMaterial> mats;
+    auto mat_id = [&](const rt_material &m) {
+        auto it = mat_ids.find(m);
+        if (it != mat_ids.end()) return it->second;
+        int id = (int)mats.size();
+        mat_ids.emplace(m, id);
+        mats.push_back(to_dev(m));
+        return id;
+    };
+
+    // Per-rank source geometry + shading record; primitives for the builder.
+    struct TriSrc { rtm::f3 v0, v1, v2; };
+    std::vector<TriSrc> tri_src((size_t)P);
+    std::vector<float4> shade((size_t)P);
+    std::vector<rtb::Prim> prims;
+    prims.reserve((size_t)P);
+    float scale = 1.0f;
+    for (float v : {smin.x, smin.y, smin.z, smax.x, smax.y, smax.z})
+        if (std::isfinite(v)) scale = std::max(scale, std::fabs(v));
+    const float pad_abs = scale * 0x1p-13f;
+    auto add_tri_prim = [&](int rank, const rt_triangle &t, int gate) {
+        rtb::Prim p;
+        const float *v[3] = {&t.vertex0.x, &t.vertex1.x, &t.vertex2.x};
+        float ext = 0.0f;
+        for (int a = 0; a < 3; ++a) {
+            p.lo[a] = std::min(v[0][a], std::min(v[1][a], v[2][a]));
+            p.hi[a] = std::max(v[0][a], std::max(v[1][a], v[2][a]));
+            ext = std::max(ext, p.hi[a] - p.lo[a]);
+        }
+        const float pad = pad_abs + ext * 1e-4f;
+        for (int a = 0; a < 3; ++a) {
+            p.c[a] = 0.5f * (p.lo[a] + p.hi[a]);
+            p.lo[a] -= pad;
+            p.hi[a] += pad;
+        }
+        p.kind = rtd::kLeafTri;
+        p.gate = gate;
+        p.payload = rank;
+        tri_src[rank] = {F3(t.vertex0), F3(t.vertex1), F3(t.vertex2)};
+        prims.push_back(p);
+    };
+    ctx->mesh_rank_first.assign((size_t)sc->mesh_count + 1, 0);
+    int rank = 0;
+    for (int m = 0; m < sc->mesh_count; ++m) {
+        const rt_mesh &M = sc->meshes[m];
+        ctx->mesh_rank_first[m] = rank;
+        const int mid = mat_id(M.material);
+        for (int i = 0; i < M.triangle_count; ++i, ++rank) {
+            const int g = M.first_triangle + i;
+            add_tri_prim(rank, sc->mesh_triangles[g], m);
+            const rt_float3 &nn = sc->mesh_triangle_normals[g];
+            int bits;
+            std::memcpy(&bits, &mid, 4);
+            shade[rank] = make_float4(nn.x, nn.y, nn.z, 0.0f);
+            std::memcpy(&shade[rank].w, &bits, 4);
+        }
+    }
+    ctx->mesh_rank_first[sc->mesh_count] = rank;
+    std::vector<rtd::SphRec> sph_src((size_t)NS);
+    for (int i = 0; i < NS; ++i, ++rank) {
+        const rt_sphere &s = sc->spheres[i];
+        const float r = sqrtf(s.radius_squared);
+        rtb::Prim p;
+        const float c[3] = {s.center.x, s.center.y, s.center.z};
+        const float pad = pad_abs + r * 1e-4f;
+        for (int a = 0; a < 3; ++a) {
+            p.c[a] = c[a];
+            p.lo[a] = c[a] - r - pad;
+            p.hi[a] = c[a] + r + pad;
+        }
+        p.kind = rtd::kLeafSphere;
+        p.gate = -1;
+        p.payload = rank;
+        prims.push_back(p);
+        sph_src[i].cr = make_float4(s.center.x, s.center.y, s.center.z, s.radius_squared);
+        sph_src[i].misc = make_int4(rank, 0, 0, 0);
+        const int mid = mat_id(sc->sphere_materials[i]);
+        shade[rank] = make_float4(s.center.x, s.center.y, s.center.z, 0.0f);
+        std::memcpy(&shade[rank].w, &mid, 4);
+    }
+    for (int i = 0; i < NL; ++i, ++rank) {
+        add_tri_prim(rank, sc->triangles[i], -1);
+        const rt_float3 &nn = sc->triangle_normals[i];
+        const int mid = mat_id(sc->triangle_materials[i]);
+        shade[rank] = make_float4(nn.x, nn.y, nn.z, 0.0f);
+        std::memcpy(&shade[rank].w, &mid, 4);
+    }
+
+    rtb::BuildResult B = rtb::build_bvh(prims, 4);
+    ctx->last_build_ms = B.build_ms;
+    ctx->last_bvh_depth = B.max_depth;
+    if (B.max_depth > rtd::kMaxTreeDepth)
+        return fail(ctx, RT_E_INTERNAL, "BVH depth %d exceeds stack", B.max_depth);
+
+    std::vector<rtd::TriRec> tris(B.tri_order.size());
+    for (size_t i = 0; i < B.tri_order.size(); ++i) {
+        const int rk = B.tri_order[i];
+        const TriSrc &t = tri_src[rk];
+        const rtm::f3 e1 = t.v1 - t.v0, e2 = t.v2 - t.v0;  // RMath.cs:34-35
+        float rbits;
+        std::memcpy(&rbits, &rk, 4);
+        tris[i].p0 = make_float4(t.v0.x, t.v0.y, t.v0.z, e1.x);
+        tris[i].p1 = make_float4(e1.y, e1.z, e2.x, e2.y);
+        tris[i].p2 = make_float4(e2.z, rbits, 0.0f, 0.0f);
+    }
+    std::vector<rtd::SphRec> sphs(B.sph_order.size());
+    for (size_t i = 0; i < B.sph_order.size(); ++i) sphs[i] = sph_src[B.sph_order[i] - MT];
+    std::vector<rtd::MeshGate> gates((size_t)sc->mesh_count);
+    for (int m = 0; m < sc->mesh_count; ++m) {
+        const rt_aabb &a = sc->meshes[m].aabb;
+        gates[m].lo = make_float4(a.min.x, a.min.y, a.min.z, 0.0f);
+        gates[m].hi = make_float4(a.max.x, a.max.y, a.max.z, 0.0f);
+    }
+    std::vector<rtd::DevLight> lights((size_t)sc->point_light_count);
+    for (int l = 0; l < sc->point_light_count; ++l) {
+        const rt_point_light &L = sc->point_lights[l];
+        lights[l].pos = make_float4(L.position.x, L.position.y, L.position.z, 0.0f);
+        lights[l].intensity = make_float4(L.intensity.x, L.intensity.y, L.intensity.z, 0.0f);
+    }
+
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.nodes, B.nodes));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.leaves, B.leaves));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.tris, tris));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.sphs, sphs));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.shade, shade));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.mats, mats));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.lights, lights));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.gates, gates));
+
+    rtd::SceneDev &S = ctx->S;
+    S.nodes = (const rtd::BvhNode *)ctx->arr.nodes;
+    S.leaves = (const rtd::LeafDesc *)ctx->arr.leaves;
+    S.tris = (const rtd::TriRec *)ctx->arr.tris;
+    S.sphs = (const rtd::SphRec *)ctx->arr.sphs;
+    S.shade = (const float4 *)ctx->arr.shade;
+    S.mats = (const rtd::DevMaterial *)ctx->arr.mats;
+    S.lights = (const rtd::DevLight *)ctx->arr.lights;
+    S.gates = (const rtd::MeshGate *)ctx->arr.gates;
+    S.num_lights = sc->point_light_count;
+    S.mesh_tri_total = MT;
+    S.sphere_count = NS;
+    S.has_prims = P > 0 && !B.nodes.empty();
+    S.scene_lo[0] = smin.x; S.scene_lo[1] = smin.y; S.scene_lo[2] = smin.z;
+    S.scene_hi[0] = smax.x; S.scene_hi[1] = smax.y; S.scene_hi[2] = smax.z;
+    S.ambient[0] = sc->ambient_radiance.x;
+    S.ambient[1] = sc->ambient_radiance.y;
+    S.ambient[2] = sc->ambient_radiance.z;
+    S.spec_threshold = spec_threshold();
+    ctx->mesh_tri_ranks = MT;
+    ctx->sphere_count = NS;
+    ctx->loose_count = NL;
+    ctx->has_scene = true;
+    return RT_OK;
+}
+
+int32_t rt_band_rows_local(int32_t resolution_y, int32_t band_index, int32_t band_count, int32_t band_rows) {
+    (void)band_index;
+    return band_local_rows(resolution_y, band_count <= 0 ? 1 : band_count, band_rows <= 0 ? 8 : band_rows);
+}
+
+int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane, const rt_render_params *params,
+              float *out_rgba, rt_stats *stats) {
+    if (!ctx) return RT_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    rtd::FrameDev F;
+    size_t bytes = 0;
+    int st = prepare_frame(ctx, camera, plane, params, F, bytes);
+    if (st) return st;
+    if (bytes && !out_rgba) return fail(ctx, RT_E_INVALID, "out_rgba is null");
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    if (bytes > ctx->d_out_cap) {
+        if (ctx->d_out) HIP_OR_FAIL(ctx, hipFree(ctx->d_out));
+        ctx->d_out = nullptr;
+        ctx->d_out_cap = 0;
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->d_out, bytes));
+        ctx->d_out_cap = bytes;
+    }
+    return run_frame(ctx, F, params, ctx->d_out, stats, t0, out_rgba, bytes);
+}
+
+int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
+                     const rt_render_params *params, float *d_out_rgba, size_t out_bytes, rt_stats *stats) {
+    if (!ctx) return RT_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    rtd::FrameDev F;
+    size_t bytes = 0;
+    int st = prepare_frame(ctx, camera, plane, params, F, bytes);
+    if (st) return st;
+    if (bytes && !d_out_rgba) return fail(ctx, RT_E_INVALID, "d_out_rgba is null");
+    if (out_bytes < bytes)
+        return fail(ctx, RT_E_INVALID, "output buffer %zu bytes < %zu required", out_bytes, bytes);
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    return run_frame(ctx, F, params, (float4 *)d_out_rgba, stats, t0, nullptr, 0);
+}
+
+int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x, int32_t resolution_y,
+                      int32_t band_count, int32_t band_rows, float *d_image) {
+    if (!ctx) return RT_E_INVALID;
+    if (!d_gathered || !d_image || resolution_x < 0 || resolution_y < 0 || band_count < 1)
+        return fail(ctx, RT_E_INVALID, "bad rt_assemble_bands arguments");
+    if (band_rows <= 0) band_rows = 8;
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    const int local = band_local_rows(resolution_y, band_count, band_rows);
+    HIP_OR_FAIL(ctx, rtk::launch_assemble((const float4 *)d_gathered, resolution_x, resolution_y, band_count,
+                                          band_rows, local, (float4 *)d_image, ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    return RT_OK;
+}
+
+int rt_intersect_rays(rt_ctx *ctx, const rt_ray *rays, int32_t n, rt_hit *out_hits) {
+    if (!ctx) return RT_E_INVALID;
+    if (n < 0 || (n > 0 && (!rays || !out_hits))) return fail(ctx, RT_E_INVALID, "bad rays/out_hits");
+    if (!ctx->has_scene) return fail(ctx, RT_E_STATE, "rt_intersect_rays before rt_set_scene");
+    if (n == 0) return RT_OK;
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    if ((size_t)n > ctx->rays_cap) {
+        if (ctx->d_rays) HIP_OR_FAIL(ctx, hipFree(ctx->d_rays));
+        if (ctx->d_hits) HIP_OR_FAIL(ctx, hipFree(ctx->d_hits));
+        ctx->d_rays = nullptr;
+        ctx->d_hits = nullptr;
+        ctx->rays_cap = 0;
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->d_rays, (size_t)n * sizeof(rt_ray)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->d_hits, (size_t)n * sizeof(int4)));
+        ctx->rays_cap = (size_t)n;
+    }
+    HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->d_rays, rays, (size_t)n * sizeof(rt_ray), hipMemcpyHostToDevice,
+                                    ctx->stream));
+    HIP_OR_FAIL(ctx, rtk::launch_intersect(ctx->S, ctx->d_rays, n, ctx->d_hits, ctx->stream));
+    std::vector<int4> hits((size_t)n);
+    HIP_OR_FAIL(ctx, hipMemcpyAsync(hits.data(), ctx->d_hits, (size_t)n * sizeof(int4), hipMemcpyDeviceToHost,
+                                    ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    for (int32_t i = 0; i < n; ++i) {
+        const int rk = hits[i].x;
+        rt_hit &h = out_hits[i];
+        std::memcpy(&h.distance, &hits[i].y, 4);
+        h.type = 0;
+        h.index = -1;
+        h.mesh_index = -1;
+        if (rk < 0) {
+            h.distance = FLT_MAX;  // float.MaxValue
+        } else if (rk < ctx->mesh_tri_ranks) {
+            const auto &f = ctx->mesh_rank_first;
+            const int m = (int)(std::upper_bound(f.begin(), f.end() - 1, rk) - f.begin()) - 1;
+            h.type = 3;
+            h.mesh_index = m;
+            h.index = rk - f[m];
+        } else if (rk < ctx->mesh_tri_ranks + ctx->sphere_count) {
+            h.type = 1;
+            h.index = rk - ctx->mesh_tri_ranks;
+        } else {
+            h.type = 2;
+            h.index = rk - ctx->mesh_tri_ranks - ctx->sphere_count;
+        }
+    }
+    return RT_OK;
+}
+
+}  // extern "C"

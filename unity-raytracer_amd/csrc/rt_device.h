@@ -1,0 +1,119 @@
+// rt_device.h — HBM layout of an uploaded scene and the kernel parameter
+// blocks.  Shared by the host (rt_abi.cpp, bvh.cpp) and the kernels.
+//
+// Layout (DESIGN.md "Data layout in HBM"):
+//   nodes   BvhNode[]   64 B  BVH2 node holding BOTH children's boxes (one
+//                             coalesced 64-B fetch tests two boxes)
+//   leaves  LeafDesc[]  16 B  {first, count, kind, gate}
+//   tris    TriRec[]    48 B  v0, edge1, edge2, rank — leaf order (Möller–
+//                             Trumbore inputs only; 3 x 16-B loads)
+//   sphs    SphRec[]    32 B  center, r^2, rank — leaf order
+//   shade   float4[]    16 B  per reference rank: normal (or sphere center),
+//                             material id — fetched once per shaded hit
+//   mats    DevMaterial 64 B  deduplicated MaterialData
+//   lights  DevLight    32 B
+//   gates   MeshGate    32 B  exact (unpadded) Mesh.AABB of every mesh
+// A "rank" is the primitive's position in the reference's scan order
+// (Scene.cs:64-115): mesh triangles (mesh by mesh), then spheres, then loose
+// triangles.  Equal distances resolve to the lowest rank, which is exactly
+// the reference's "first wins" (strict '>', Scene.cs:75,93,108).
+#pragma once
+
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace rtd {
+
+constexpr int kStackSize = 32;      // LDS traversal stack entries per lane
+constexpr int kMaxTreeDepth = 31;   // builder guarantees internal depth < kStackSize
+constexpr int kMaxBounces = 32;     // per-lane mirror fold stack
+constexpr int kWaveSize = 64;
+constexpr int kBlockThreads = 256;  // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;
+
+constexpr int kLeafTri = 0;
+constexpr int kLeafSphere = 1;
+
+struct alignas(16) BvhNode {
+    float4 a;  // child0 lo.x, hi.x, lo.y, hi.y
+    float4 b;  // child1 lo.x, hi.x, lo.y, hi.y
+    float4 c;  // child0 lo.z, hi.z, child1 lo.z, hi.z
+    int4 d;    // child0, child1 (>= 0 internal node, < 0 leaf ~index), unused
+};
+
+struct alignas(16) LeafDesc {
+    int first;  // into tris[] or sphs[]
+    int count;
+    int kind;   // kLeafTri / kLeafSphere
+    int gate;   // mesh index whose exact AABB gates this leaf, -1 = none
+};
+
+struct alignas(16) TriRec {
+    float4 p0;  // v0.x v0.y v0.z e1.x
+    float4 p1;  // e1.y e1.z e2.x e2.y
+    float4 p2;  // e2.z rank(bits) - -
+};
+
+struct alignas(16) SphRec {
+    float4 cr;  // center.xyz, radius_squared
+    int4 misc;  // rank, -, -, -
+};
+
+struct alignas(16) DevMaterial {
+    float4 kd_phong;   // DiffuseReflectance.xyz, PhongExponent
+    float4 ka_mirror;  // AmbientReflectance.xyz, IsMirror (0/1 as float)
+    float4 km;         // MirrorReflectance.xyz, -
+    float4 ks;         // SpecularReflectance.xyz, -
+};
+
+struct alignas(16) DevLight {
+    float4 pos;        // Position.xyz
+    float4 intensity;  // Intensity.xyz
+};
+
+struct alignas(16) MeshGate {
+    float4 lo;
+    float4 hi;
+};
+
+// Everything a kernel needs to read the scene.
+struct SceneDev {
+    const BvhNode *nodes;
+    const LeafDesc *leaves;
+    const TriRec *tris;
+    const SphRec *sphs;
+    const float4 *shade;
+    const DevMaterial *mats;
+    const DevLight *lights;
+    const MeshGate *gates;
+    int num_lights;
+    int mesh_tri_total;  // ranks [0, mesh_tri_total) are mesh triangles
+    int sphere_count;    // ranks [mesh_tri_total, +sphere_count) are spheres
+    int has_prims;       // 0 → every ray misses after the scene gate
+    float scene_lo[3];   // Scene.AABB (Scene.CalculateAABB)
+    float scene_hi[3];
+    float ambient[3];    // AmbientLight.Radiance
+    float spec_threshold;  // d < spec_threshold  <=>  degrees(acos(d)) > 90f
+};
+
+// Per-frame constants of CastPixelRays (RayTracingSetup.cs:277-284).
+struct FrameDev {
+    float cam_pos[3];
+    float right[3];
+    float up[3];
+    float top_left[3];       // ImagePlane.GetRect(camera).TopLeft
+    float hl, vl;            // HorizontalLength, VerticalLength
+    float bg255[3];          // new Rgb(BackgroundColor).Value
+    int res_x, res_y;
+    int spp, spp_n;          // samples per pixel = spp_n * spp_n
+    int max_bounces;
+    int band_index, band_count, band_rows;
+    int local_rows;          // rows of the compact output buffer
+    int tile_w, tile_h;      // pixels of one wave's tile
+    int tiles_x, num_tiles;
+    float4 *out;             // local_rows x res_x RGBA
+    unsigned long long *counters;  // 7 x u64, rt_stats order
+};
+
+}  // namespace rtd

@@ -1,0 +1,172 @@
+"""Host-side mirror of the reference's RayTracingSetup render interface.
+
+The reference seam is the private ``RayTracingSetup.CastPixelRays(CameraData)``
+(Assets/RayTracer/Demo-RayTracing/RayTracingSetup.cs:275-302), reading the
+serialized fields ``ImagePlane`` (:21), ``BackgroundColor`` (:22),
+``MaxReflectionBounces`` (:23) and ``Scene`` (:38) and writing
+``PixelColors`` (:40).  ``RayTracingSetup`` below keeps those names and
+meanings and drives the MI355X C-ABI (include/rt_mi355.h); there is no CPU
+path: constructing it without the HIP library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Optional
+
+import numpy as np
+
+from . import abi
+from .scene import Scene
+from .scenes import CameraData, Frame, ImagePlane
+
+
+def camera_struct(cam: CameraData) -> abi.rt_camera:
+    return abi.rt_camera(abi.f3(cam.Position), abi.f3(cam.Forward), abi.f3(cam.Right), abi.f3(cam.Up))
+
+
+def plane_struct(p: ImagePlane) -> abi.rt_image_plane:
+    return abi.rt_image_plane(int(p.ResolutionX), int(p.ResolutionY), float(p.DistanceToCamera),
+                              float(p.HalfHorizontalLength), float(p.HalfVerticalLength))
+
+
+def params_struct(background=(0, 0, 0, 1), max_bounces=0, spp=1, band_index=0, band_count=1,
+                  band_rows=8, flags=0) -> abi.rt_render_params:
+    p = abi.rt_render_params()
+    for i in range(4):
+        p.background_color[i] = float(background[i])
+    p.max_reflection_bounces = int(max_bounces)
+    p.samples_per_pixel = int(spp)
+    p.band_index = int(band_index)
+    p.band_count = int(band_count)
+    p.band_rows = int(band_rows)
+    p.flags = int(flags)
+    return p
+
+
+def frame_params(fr: Frame, **kw) -> abi.rt_render_params:
+    return params_struct(fr.background, fr.max_bounces, kw.pop("spp", fr.spp), **kw)
+
+
+class Context:
+    """Owns one rt_ctx (one GPU).  Thin, error-checked wrapper of the C-ABI."""
+
+    def __init__(self, num_gpus: int = 1, lib_path: Optional[str] = None):
+        self.lib = abi.load_library(lib_path)
+        h = C.c_void_p()
+        st = self.lib.rt_create(C.byref(h), int(num_gpus))
+        if st != abi.RT_OK:
+            raise abi.RtError(st, self.lib.rt_last_error(None).decode())
+        self.h = h
+        self._scene_desc = None
+
+    def _check(self, st: int):
+        if st != abi.RT_OK:
+            raise abi.RtError(st, self.lib.rt_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int):
+        self._check(self.lib.rt_set_stream(self.h, C.c_void_p(stream_handle)))
+
+    def set_scene(self, scene: Scene):
+        desc = scene.to_desc()
+        self._check(self.lib.rt_set_scene(self.h, desc.ref()))
+        self._scene_desc = desc  # keep arrays alive for the duration of the call only; harmless
+
+    def render(self, camera: CameraData, plane: ImagePlane, params: abi.rt_render_params,
+               out: Optional[np.ndarray] = None):
+        rows = plane.ResolutionY
+        if params.band_count > 1:
+            rows = self.lib.rt_band_rows_local(plane.ResolutionY, params.band_index,
+                                               params.band_count, params.band_rows)
+        if out is None:
+            out = np.empty((rows, plane.ResolutionX, 4), np.float32)
+        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size >= rows * plane.ResolutionX * 4
+        stats = abi.rt_stats()
+        cam, pl = camera_struct(camera), plane_struct(plane)
+        self._check(self.lib.rt_render(self.h, C.byref(cam), C.byref(pl), C.byref(params),
+                                       out.ctypes.data_as(C.c_void_p), C.byref(stats)))
+        return out, stats
+
+    def render_device(self, camera: CameraData, plane: ImagePlane, params: abi.rt_render_params,
+                      dev_ptr: int, nbytes: int):
+        stats = abi.rt_stats()
+        cam, pl = camera_struct(camera), plane_struct(plane)
+        self._check(self.lib.rt_render_device(self.h, C.byref(cam), C.byref(pl), C.byref(params),
+                                              C.c_void_p(dev_ptr), C.c_size_t(nbytes), C.byref(stats)))
+        return stats
+
+    def assemble_bands(self, gathered_ptr: int, res_x: int, res_y: int, band_count: int,
+                       band_rows: int, image_ptr: int):
+        self._check(self.lib.rt_assemble_bands(self.h, C.c_void_p(gathered_ptr), res_x, res_y,
+                                               band_count, band_rows, C.c_void_p(image_ptr)))
+
+    def intersect_rays(self, rays: np.ndarray) -> np.ndarray:
+        """Scene.IntersectRay (Scene.cs:43-122) for (N, 6) float32 rays;
+        returns a structured array (type, index, mesh_index, distance)."""
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+        out = np.zeros(len(rays), HIT_DTYPE)
+        self._check(self.lib.rt_intersect_rays(self.h, rays.ctypes.data_as(C.c_void_p), len(rays),
+                                               out.ctypes.data_as(C.c_void_p)))
+        return out
+
+
+HIT_DTYPE = np.dtype([("type", np.int32), ("index", np.int32), ("mesh_index", np.int32),
+                      ("distance", np.float32)])
+
+
+class RayTracingSetup:
+    """Mirror of RayTracingSetup's render part (RayTracingSetup.cs:19-40,275-302).
+
+    Fields keep the reference's names: ImagePlane, BackgroundColor,
+    MaxReflectionBounces, Scene, PixelColors.  SamplesPerPixel is the
+    documented n*n extension (1 == reference)."""
+
+    def __init__(self, scene: Scene, image_plane: ImagePlane, background_color=(0, 0, 0, 1),
+                 max_reflection_bounces: int = 0, samples_per_pixel: int = 1,
+                 context: Optional[Context] = None):
+        self.Scene = scene
+        self.ImagePlane = image_plane
+        self.BackgroundColor = tuple(background_color)
+        self.MaxReflectionBounces = int(max_reflection_bounces)
+        self.SamplesPerPixel = int(samples_per_pixel)
+        self.PixelColors = np.zeros((0, 4), np.float32)
+        self.ctx = context or Context()
+        self.LastStats: Optional[abi.rt_stats] = None
+        self.UpdateScene()
+
+    @classmethod
+    def from_frame(cls, fr: Frame, context: Optional[Context] = None) -> "RayTracingSetup":
+        return cls(fr.scene, fr.plane, fr.background, fr.max_bounces, fr.spp, context)
+
+    def UpdateScene(self):
+        """Upload Scene (replaces UpdateScene()'s result, :120-128; the
+        library computes Scene.CalculateAABB and the BVH)."""
+        self.ctx.set_scene(self.Scene)
+
+    def CastPixelRays(self, camera: CameraData, flags: int = 0) -> np.ndarray:
+        """:275-302 — fills PixelColors (resX*resY RGBA, index x + y*resX)."""
+        p = self.ImagePlane
+        params = params_struct(self.BackgroundColor, self.MaxReflectionBounces, self.SamplesPerPixel,
+                               flags=flags)
+        img, stats = self.ctx.render(camera, p, params)
+        self.PixelColors = img.reshape(-1, 4)
+        self.LastStats = stats
+        return self.PixelColors
+
+
+def spp_side(spp: int) -> int:
+    n = int(math.isqrt(spp))
+    if n * n != spp or n < 1:
+        raise ValueError(f"samples_per_pixel must be n*n, got {spp}")
+    return n
