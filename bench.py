@@ -1,0 +1,207 @@
+"""bench.py — Mrays/s and ms/frame of the MI355X trace path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = one frame of the BASELINE.json metric config (C3: 69,132-tri BVH
+scene, 1920x1080, 4 spp, depth 8) rendered through the C-ABI with the scene
+already resident in HBM and the frame left in HBM.  With N > 1 ranks the
+frame's rows are block-cyclic sharded (band_index = rank) and the shards are
+gathered to rank 0 over RCCL and reassembled by a HIP kernel — the fixed
+frame is split, so scaling is "strong".  value = rays traced by all ranks
+(primary + shadow + reflection, counted on device) / max-over-ranks time.
+
+Rank 0 prints ONE JSON line with a roofline object for the trace kernel and
+a cpu_baseline measured with the C oracle (single-thread brute force, the
+reference's algorithm) on a bounded pixel sample of the same frame.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before the HIP library: one HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+import _rt_pkg  # noqa: E402
+
+METRIC = "Mrays/sec + ms/frame at 1920x1080, 4spp, depth 8; 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+
+
+def algorithmic_bytes(st, res_x, local_rows):
+    """B = 32*N_box + 36*N_tri + 16*N_sph + 16*N_hit + 16*W*H."""
+    return (32 * st.box_tests + 36 * st.triangle_tests + 16 * st.sphere_tests
+            + 16 * st.shading_fetches + 16 * res_x * local_rows)
+
+
+def cpu_baseline(rt, fr, budget_s):
+    """Single-thread brute-force oracle (the reference's algorithm, which is
+    single-threaded Mono C#) on seeded random pixels of the same frame,
+    until budget_s of CPU time: returns Mrays/s (same ray accounting)."""
+    orc = _rt_pkg.load_oracle()
+    rng = np.random.default_rng(20250101)
+    total = fr.plane.ResolutionX * fr.plane.ResolutionY
+    rays, secs, pixels = 0, 0.0, 0
+    batch = 8
+    while secs < budget_s:
+        idx = rng.integers(0, total, batch).astype(np.int32)
+        t0 = time.perf_counter()
+        _, c = orc.render_pixels(fr, idx, threads=1)
+        secs += time.perf_counter() - t0
+        rays += c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
+        pixels += batch
+    return {
+        "value": rays / secs / 1e6,
+        "unit": "Mrays/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{pixels} seeded random pixels of {fr.name} ({fr.spp} spp, depth {fr.max_bounces}), "
+                  f"{rays} rays in {secs:.1f} s, brute-force C oracle (oracle/rt_oracle.c), 1 thread",
+    }
+
+
+def load_traffic(config):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p)).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+
+    rt = _rt_pkg.load()
+    fr = rt.make(args.config)
+    ctx = rt.Context()
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream.cuda_stream)
+    ctx.set_scene(fr.scene)
+    rx, ry = fr.plane.ResolutionX, fr.plane.ResolutionY
+    R = 8
+    band_count = world
+    local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if world > 1 else ry
+    out = torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda")
+    nbytes = out.numel() * 4
+    params = rt.frame_params(fr, band_index=rank if world > 1 else 0, band_count=band_count, band_rows=R)
+    if world > 1:
+        gathered = torch.empty((world, local_rows, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+        image = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+
+    def step():
+        st = ctx.render_device(fr.camera, fr.plane, params, out.data_ptr(), nbytes)
+        if world > 1:
+            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                ctx.assemble_bands(gathered.data_ptr(), rx, ry, world, R, image.data_ptr())
+        return st
+
+    # counting launch (untimed): algorithmic work of this rank's frame
+    cparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
+                              flags=rt.abi.RT_FLAG_COUNT_TESTS)
+    cst = ctx.render_device(fr.camera, fr.plane, cparams, out.data_ptr(), nbytes)
+    bytes_per_launch = algorithmic_bytes(cst, rx, local_rows)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rays = 0
+    kernel_ms = 0.0
+    for _ in range(args.steps):
+        st = step()
+        rays += st.primary_rays + st.shadow_rays + st.reflection_rays
+        kernel_ms += st.kernel_ms
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    if world > 1:
+        t = torch.tensor([elapsed, float(rays), kernel_ms], dtype=torch.float64, device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+        rays = int(t[1])
+        kernel_ms_max = float(tmax[2])
+    else:
+        kernel_ms_max = kernel_ms
+
+    if rank == 0:
+        avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's own trace kernel, HIP events
+        achieved = bytes_per_launch / avg_kernel_s / 1e9
+        line = {
+            "metric": METRIC,
+            "value": rays / elapsed / 1e6,
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{fr.name}: {fr.scene.triangle_count}-triangle BVH scene (procedural torus-knot "
+                            f"stand-in for the ~69k-tri bunny), {rx}x{ry}, {fr.spp} spp, depth {fr.max_bounces}",
+                "resolution": f"{rx}x{ry}",
+                "spp": fr.spp,
+                "depth": fr.max_bounces,
+                "triangles": fr.scene.triangle_count,
+                "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "rays_per_frame": rays // args.steps,
+                "kernel_ms_per_frame": kernel_ms_max / args.steps,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic(args.config),
+                "kernel": "render_kernel<false>",
+                "bytes_per_launch": bytes_per_launch,
+                "avg_kernel_ms": avg_kernel_s * 1e3,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(rt, fr, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,12 @@ class orc_counts(C.Structure):
 _lib = None
 
 
+def default_threads() -> int:
+    """Host threads for the oracle: OMP_NUM_THREADS (16 on the GPU box), capped at 16."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    return max(1, min(16, n))
+
+
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
@@ -121,7 +127,7 @@ def render(fr, threads: int = 0, spp=None):
     out = np.zeros((fr.plane.ResolutionY, fr.plane.ResolutionX, 4), np.float32)
     cnt = orc_counts()
     st = lib().orc_render(C.cast(d.ref(), C.c_void_p), C.byref(cam), C.byref(pl), C.byref(prm),
-                          _p(out), C.byref(cnt), threads or os.cpu_count())
+                          _p(out), C.byref(cnt), threads or default_threads())
     if st != 0:
         raise RuntimeError(f"oracle render failed: {st}")
     return out, cnt.as_dict()
@@ -134,7 +140,7 @@ def render_pixels(fr, pixel_indices, threads: int = 0, spp=None):
     out = np.zeros((len(idx), 4), np.float32)
     cnt = orc_counts()
     st = lib().orc_render_pixels(C.cast(d.ref(), C.c_void_p), C.byref(cam), C.byref(pl), C.byref(prm),
-                                 _p(idx), len(idx), _p(out), C.byref(cnt), threads or os.cpu_count())
+                                 _p(idx), len(idx), _p(out), C.byref(cnt), threads or default_threads())
     if st != 0:
         raise RuntimeError(f"oracle render failed: {st}")
     return out, cnt.as_dict()
@@ -147,7 +153,7 @@ def render_rows(fr, row_start, row_step, threads: int = 0, spp=None):
     out = np.zeros((nrows, fr.plane.ResolutionX, 4), np.float32)
     cnt = orc_counts()
     st = lib().orc_render_rows(C.cast(d.ref(), C.c_void_p), C.byref(cam), C.byref(pl), C.byref(prm),
-                               row_start, row_step, _p(out), C.byref(cnt), threads or os.cpu_count())
+                               row_start, row_step, _p(out), C.byref(cnt), threads or default_threads())
     if st != 0:
         raise RuntimeError(f"oracle render failed: {st}")
     return out, cnt.as_dict()
