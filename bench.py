@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=["wavefront", "megakernel"], default="wavefront")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,7 +110,9 @@ def main():
     local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if world > 1 else ry
     out = torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda")
     nbytes = out.numel() * 4
-    params = rt.frame_params(fr, band_index=rank if world > 1 else 0, band_count=band_count, band_rows=R)
+    mode_flags = rt.abi.RT_FLAG_MEGAKERNEL if args.mode == "megakernel" else 0
+    params = rt.frame_params(fr, band_index=rank if world > 1 else 0, band_count=band_count, band_rows=R,
+                             flags=mode_flags)
     if world > 1:
         gathered = torch.empty((world, local_rows, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
         image = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
@@ -124,7 +127,7 @@ def main():
 
     # counting launch (untimed): algorithmic work of this rank's frame
     cparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
-                              flags=rt.abi.RT_FLAG_COUNT_TESTS)
+                              flags=rt.abi.RT_FLAG_COUNT_TESTS | mode_flags)
     cst = ctx.render_device(fr.camera, fr.plane, cparams, out.data_ptr(), nbytes)
     bytes_per_launch = algorithmic_bytes(cst, rx, local_rows)
 
@@ -190,7 +193,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": load_traffic(args.config),
-                "kernel": "render_kernel<false>",
+                "kernel": "render_kernel<false>" if args.mode == "megakernel" else "wavefront passes (sum)",
                 "bytes_per_launch": bytes_per_launch,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
             },

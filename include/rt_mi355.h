@@ -141,6 +141,7 @@ typedef struct rt_render_params {
 } rt_render_params;
 
 #define RT_FLAG_COUNT_TESTS 1   /* fill rt_stats box/triangle/sphere counters (slower) */
+#define RT_FLAG_MEGAKERNEL  2   /* one-launch megakernel instead of the wavefront passes */
 
 /* Work counters and timings of the last render. */
 typedef struct rt_stats {

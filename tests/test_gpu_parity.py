@@ -30,6 +30,10 @@ def _check(img, ref, st, counts, name):
     assert got == want, f"{name}: ray counts {got} != oracle {want}"
 
 
+MODES = {"wavefront": 0, "megakernel": 2}  # rt_render_params.flags (RT_FLAG_MEGAKERNEL)
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("name,res,spp", [
     ("demo", None, 1),
     ("C1", None, 1),
@@ -38,14 +42,25 @@ def _check(img, ref, st, counts, name):
     ("C3", (96, 54), 4),
     ("C5", (48, 27), 4),
 ])
-def test_frame_vs_oracle(gpu_ctx, rt, orc, name, res, spp):
+def test_frame_vs_oracle(gpu_ctx, rt, orc, name, res, spp, mode):
     fr = rt.make(name)
     if res:
         fr = fr.with_resolution(*res)
     fr = fr.with_(spp=spp)
-    img, st = _render(gpu_ctx, rt, fr)
+    img, st = _render(gpu_ctx, rt, fr, flags=MODES[mode])
     ref, counts = orc.render(fr)
-    _check(img, ref, st, counts, name)
+    _check(img, ref, st, counts, f"{name}/{mode}")
+
+
+def test_modes_bit_identical_full_c3(gpu_ctx, rt):
+    """Wavefront and megakernel frames are bit-identical at full C3 size, and
+    so are their ray counts."""
+    fr = rt.make("C3")
+    a, sa = _render(gpu_ctx, rt, fr, flags=0)
+    b, sb = _render(gpu_ctx, rt, fr, flags=2)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert (sa.primary_rays, sa.shadow_rays, sa.reflection_rays) == (sb.primary_rays, sb.shadow_rays,
+                                                                     sb.reflection_rays)
 
 
 def test_goldens(gpu_ctx, rt):

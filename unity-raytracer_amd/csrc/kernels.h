@@ -4,12 +4,19 @@
 #include <hip/hip_runtime.h>
 
 #include "rt_device.h"
+#include "wavefront.h"
 
 namespace rtk {
 
 // One frame (or one row shard of it): CastPixelRays + Shade, RayTracingSetup.cs:275-366.
-hipError_t launch_render(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
-                         hipStream_t stream);
+// Megakernel: one lane per sample, whole Whitted chain in one launch (trace.hip).
+hipError_t launch_render_mega(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
+                              hipStream_t stream);
+
+// Wavefront: per-level queues in HBM, persistent traversal with dynamic ray
+// fetch (trace_wf.hip); chunk_tiles tiles (64 slots each) per pass sequence.
+hipError_t launch_render_wavefront(const rtd::SceneDev &S, const rtd::FrameDev &F, const rtw::Args &A,
+                                   int chunk_tiles, bool count_tests, hipStream_t stream);
 
 // Batch closest hit, Scene.IntersectRay (Scene.cs:43-122): rays are 6 floats
 // (origin, direction); out[i] = {rank or -1, distance bits, -, -}.

@@ -52,6 +52,12 @@ struct rt_ctx {
     int4 *d_hits = nullptr;
     size_t rays_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // wavefront queues (trace_wf.hip); pool_cap entries, shadow_cap shadow rays
+    rtw::Counters *wf_ctr = nullptr;
+    float4 *wf_ray_o = nullptr, *wf_ray_d = nullptr, *wf_col = nullptr, *wf_sh_o = nullptr, *wf_sh_d = nullptr;
+    int4 *wf_hit = nullptr;
+    unsigned char *wf_occ = nullptr;
+    size_t pool_cap = 0, shadow_cap = 0;
     double last_build_ms = 0.0;
     int last_bvh_depth = 0;
 };
@@ -219,13 +225,77 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     return RT_OK;
 }
 
+// Upper bound on wavefront pool entries (64 B each) per chunk: 160M = 10 GB.
+constexpr size_t kPoolBudget = (size_t)160 << 20;
+constexpr size_t kShadowBudget = (size_t)96 << 20;
+
+void free_wavefront(rt_ctx *c) {
+    void *ps[] = {c->wf_ray_o, c->wf_ray_d, c->wf_col, c->wf_sh_o, c->wf_sh_d, c->wf_hit, c->wf_occ};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    c->wf_ray_o = c->wf_ray_d = c->wf_col = c->wf_sh_o = c->wf_sh_d = nullptr;
+    c->wf_hit = nullptr;
+    c->wf_occ = nullptr;
+    c->pool_cap = c->shadow_cap = 0;
+}
+
+// Chunk size (tiles) so that the worst case (every hit a mirror down to the
+// bounce limit) fits the pool budget, and (re)allocation of the queues.
+int prepare_wavefront(rt_ctx *ctx, const rtd::FrameDev &F, int &chunk_tiles, rtw::Args &A) {
+    const size_t levels = (size_t)(F.max_bounces > 0 ? F.max_bounces : 0) + 1;
+    const size_t lights = (size_t)std::max(1, ctx->S.num_lights);
+    size_t tiles = (size_t)std::max(1, F.num_tiles);
+    tiles = std::min(tiles, std::max<size_t>(1, kPoolBudget / (levels * 64)));
+    tiles = std::min(tiles, std::max<size_t>(1, kShadowBudget / (lights * 64)));
+    chunk_tiles = (int)tiles;
+    const size_t pool = tiles * 64 * levels, shadow = tiles * 64 * lights;
+    if (!ctx->wf_ctr) HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ctr, sizeof(rtw::Counters)));
+    if (pool > ctx->pool_cap || shadow > ctx->shadow_cap) {
+        HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+        free_wavefront(ctx);
+        const size_t p = std::max(pool, ctx->pool_cap), q = std::max(shadow, ctx->shadow_cap);
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ray_o, p * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ray_d, p * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_col, p * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_hit, p * sizeof(int4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_sh_o, q * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_sh_d, q * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_occ, q));
+        ctx->pool_cap = p;
+        ctx->shadow_cap = q;
+    }
+    A.ctr = ctx->wf_ctr;
+    A.ray_o = ctx->wf_ray_o;
+    A.ray_d = ctx->wf_ray_d;
+    A.hit = ctx->wf_hit;
+    A.col = ctx->wf_col;
+    A.sh_o = ctx->wf_sh_o;
+    A.sh_d = ctx->wf_sh_d;
+    A.occ = ctx->wf_occ;
+    A.tile0 = 0;
+    A.n0 = 0;
+    A.max_level = (int)levels - 1;
+    return RT_OK;
+}
+
 int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, float4 *d_out, rt_stats *stats,
               std::chrono::steady_clock::time_point t_start, float *host_out, size_t out_bytes) {
     F.out = d_out;
     F.counters = ctx->d_counters;
+    const bool count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
+    const bool mega = (prm->flags & RT_FLAG_MEGAKERNEL) != 0;
+    int chunk_tiles = 0;
+    rtw::Args A{};
+    if (!mega && F.num_tiles > 0) {
+        int st = prepare_wavefront(ctx, F, chunk_tiles, A);
+        if (st) return st;
+    }
     HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(unsigned long long), ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    HIP_OR_FAIL(ctx, rtk::launch_render(ctx->S, F, (prm->flags & RT_FLAG_COUNT_TESTS) != 0, ctx->stream));
+    if (mega)
+        HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, count, ctx->stream));
+    else if (F.num_tiles > 0)
+        HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, count, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     unsigned long long counts[8] = {0};
     HIP_OR_FAIL(ctx, hipMemcpyAsync(counts, ctx->d_counters, sizeof counts, hipMemcpyDeviceToHost, ctx->stream));
@@ -292,6 +362,8 @@ void rt_destroy(rt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
+    free_wavefront(ctx);
+    if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_rays) (void)hipFree(ctx->d_rays);

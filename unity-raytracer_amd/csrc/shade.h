@@ -1,0 +1,115 @@
+// shade.h — Whitted shading of one hit, RayTracingSetup.cs:304-455, split
+// into the pieces the megakernel and the wavefront kernels share.  Every
+// function recomputes from (ray, t, rank) with the same operations, so the
+// wavefront "shade" and "finish" passes see bit-identical P, N, V, L.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_device.h"
+#include "rt_math.h"
+#include "traverse.h"
+
+namespace rts {
+
+using rtm::f3;
+using rtm::mk;
+
+struct Surface {
+    f3 p;     // surfacePoint = Ray.GetPoint(t), Ray.cs:18-21
+    f3 n;     // GetSurfaceNormalAndMaterial, :409-436
+    f3 view;  // rayDirection = normalize(rayOrigin - surfacePoint), :325
+    int mat;
+};
+
+__device__ __forceinline__ Surface surface(const rtd::SceneDev &S, f3 o, f3 d, float t, int rank) {
+    Surface s;
+    s.p = o + d * t;
+    const float4 sh = S.shade[rank];
+    s.mat = __float_as_int(sh.w);
+    if (rank >= S.mesh_tri_total && rank < S.mesh_tri_total + S.sphere_count)
+        s.n = rtm::normalize(s.p - mk(sh.x, sh.y, sh.z));  // GetSphereNormal :402-407
+    else
+        s.n = mk(sh.x, sh.y, sh.z);  // TriangleData.Normals (:422) / Mesh.TriangleNormals (:428)
+    s.view = rtm::normalize(o - s.p);
+    return s;
+}
+
+// CalculateAmbient :438-441
+__device__ __forceinline__ f3 ambient(const rtd::SceneDev &S, const rtd::DevMaterial &m) {
+    return rtt::ld3(S.ambient) * mk(m.ka_mirror.x, m.ka_mirror.y, m.ka_mirror.z);
+}
+
+struct ShadowRay {
+    f3 o, dir;
+    float d2;  // lightDistanceSq = distancesq(P, L) = lengthsq(L - P)
+};
+
+// :329-334
+__device__ __forceinline__ ShadowRay shadow_ray(const Surface &s, const rtd::DevLight &L) {
+    ShadowRay r;
+    const f3 lmp = mk(L.pos.x, L.pos.y, L.pos.z) - s.p;
+    r.dir = rtm::normalize(lmp);
+    r.o = s.p + s.n * rtm::kShadowEpsilon;
+    r.d2 = rtm::dot(lmp, lmp);
+    return r;
+}
+
+// diffuseRgb + specularRgb of one unoccluded light (:350-355).
+__device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &s, const rtd::DevMaterial &m,
+                                         const rtd::DevLight &L, const ShadowRay &sr) {
+    const f3 e = mk(L.intensity.x, L.intensity.y, L.intensity.z) / sr.d2;  // receivedIrradiance :350
+    const float ldn = rtm::dot(sr.dir, s.n);
+    const f3 kd = mk(m.kd_phong.x, m.kd_phong.y, m.kd_phong.z);
+    const f3 diffuse = (kd * rtm::umax(0.0f, ldn)) * e;  // CalculateDiffuse :443-455
+    f3 spec = mk(0.0f, 0.0f, 0.0f);
+    // CalculateSpecular :375-400: degrees(acos(ldn)) > 90f  <=>  ldn < threshold
+    if (!(ldn < S.spec_threshold)) {
+        const f3 v = sr.dir + s.view;
+        const f3 h = v / rtm::length(v);
+        const float cnh = rtm::umax(0.0f, rtm::dot(s.n, h));
+        // pow(float, float) = (float)System.Math.Pow((double)x, (double)y)
+        const float pw = (float)pow((double)cnh, (double)m.kd_phong.w);
+        spec = (mk(m.ks.x, m.ks.y, m.ks.z) * pw) * e;
+    }
+    return diffuse + spec;
+}
+
+// Reflect :368-373 (direction not re-normalised)
+__device__ __forceinline__ void reflect(const Surface &s, f3 &o, f3 &d) {
+    o = s.p + s.n * rtm::kShadowEpsilon;
+    d = ((2.0f * s.n) * rtm::dot(s.view, s.n)) - s.view;
+}
+
+// Primary ray of sample (px, gy, sub-sample s): CastPixelRays :291-298 with
+// n*n stratified offsets ((i + 0.5) / n; n == 1 gives the reference's 0.5).
+__device__ __forceinline__ void primary_ray(const rtd::FrameDev &F, int px, int gy, int s, f3 &o, f3 &d) {
+    const int n = F.spp_n;
+    const int sj = s / n, si = s - sj * n;
+    const float ox = ((float)si + 0.5f) / (float)n;
+    const float oy = ((float)sj + 0.5f) / (float)n;
+    const float rm = (((float)px + ox) * F.hl) / (float)F.res_x;
+    const float dm = (((float)gy + oy) * F.vl) / (float)F.res_y;
+    const f3 pp = (rtt::ld3(F.top_left) + rm * rtt::ld3(F.right)) - rtt::ld3(F.up) * dm;
+    o = rtt::ld3(F.cam_pos);
+    d = rtm::normalize(pp - o);
+}
+
+// Slot (tile, lane) -> pixel; false for lanes outside the image/shard.
+__device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int lane, int &px, int &ly, int &gy,
+                                           int &s) {
+    const int spp = F.spp;
+    const int pix = lane / spp;
+    s = lane - pix * spp;
+    const int tx = tile % F.tiles_x, ty = tile / F.tiles_x;
+    px = tx * F.tile_w + pix % F.tile_w;
+    ly = ty * F.tile_h + pix / F.tile_w;
+    gy = ly;
+    if (F.band_count > 1) {
+        const int blk = ly / F.band_rows;
+        gy = (blk * F.band_count + F.band_index) * F.band_rows + (ly - blk * F.band_rows);
+    }
+    return pix < F.tile_w * F.tile_h && px < F.res_x && ly < F.local_rows && gy < F.res_y;
+}
+
+}  // namespace rts

@@ -1,0 +1,224 @@
+// traverse.h — device-side BVH traversal shared by the megakernel
+// (trace.hip) and the wavefront kernels (trace_wf.hip).
+//
+// Scene.IntersectRay (Data/Objects/Scene.cs:43-122) over the BVH of
+// rt_device.h.  Results equal the brute-force scan: same candidate set (the
+// exact scene and per-mesh AABB gates, padded node boxes), same winner
+// (lowest distance, ties to the lowest reference rank).
+#pragma once
+
+#include <float.h>
+
+#include <hip/hip_runtime.h>
+
+#include "rt_device.h"
+#include "rt_math.h"
+
+namespace rtt {
+
+using rtd::kWaveSize;
+using rtm::f3;
+using rtm::mk;
+
+struct Counts {
+    unsigned primary, shadow, reflection, box, tri, sph, shading;
+};
+
+struct RayCtx {
+    f3 o, d;  // exact ray (reference semantics)
+    f3 inv;   // rcp(dir) = 1.0f / dir, exact — the reference's AABB gates
+    f3 ninv;  // node-test inverse (zero components nudged, approximate rcp)
+    f3 noi;   // o * ninv
+};
+
+__device__ __forceinline__ float nudge(float v) { return fabsf(v) > 1e-20f ? v : copysignf(1e-20f, v); }
+
+__device__ __forceinline__ void setup_ray(RayCtx &r, f3 o, f3 d) {
+    r.o = o;
+    r.d = d;
+    r.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.ninv = mk(__builtin_amdgcn_rcpf(nudge(d.x)), __builtin_amdgcn_rcpf(nudge(d.y)),
+                __builtin_amdgcn_rcpf(nudge(d.z)));
+    r.noi = mk(o.x * r.ninv.x, o.y * r.ninv.y, o.z * r.ninv.z);
+}
+
+__device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+
+// Conservative slab test of both children of a node (padded boxes; FMA form).
+__device__ __forceinline__ void test_children(const float4 a, const float4 b, const float4 c, const RayCtx &r,
+                                              float tcull, bool &h0, bool &h1, float &tn0, float &tn1) {
+    const float l0x = fmaf(a.x, r.ninv.x, -r.noi.x), u0x = fmaf(a.y, r.ninv.x, -r.noi.x);
+    const float l0y = fmaf(a.z, r.ninv.y, -r.noi.y), u0y = fmaf(a.w, r.ninv.y, -r.noi.y);
+    const float l0z = fmaf(c.x, r.ninv.z, -r.noi.z), u0z = fmaf(c.y, r.ninv.z, -r.noi.z);
+    const float l1x = fmaf(b.x, r.ninv.x, -r.noi.x), u1x = fmaf(b.y, r.ninv.x, -r.noi.x);
+    const float l1y = fmaf(b.z, r.ninv.y, -r.noi.y), u1y = fmaf(b.w, r.ninv.y, -r.noi.y);
+    const float l1z = fmaf(c.z, r.ninv.z, -r.noi.z), u1z = fmaf(c.w, r.ninv.z, -r.noi.z);
+    tn0 = fmaxf(fmaxf(fminf(l0x, u0x), fminf(l0y, u0y)), fmaxf(fminf(l0z, u0z), 0.0f));
+    const float tf0 = fminf(fminf(fmaxf(l0x, u0x), fmaxf(l0y, u0y)), fminf(fmaxf(l0z, u0z), tcull));
+    tn1 = fmaxf(fmaxf(fminf(l1x, u1x), fminf(l1y, u1y)), fmaxf(fminf(l1z, u1z), 0.0f));
+    const float tf1 = fminf(fminf(fmaxf(l1x, u1x), fmaxf(l1y, u1y)), fminf(fmaxf(l1z, u1z), tcull));
+    h0 = tn0 <= tf0;
+    h1 = tn1 <= tf1;
+}
+
+// Resumable traversal state of one lane.
+struct Trav {
+    int node;         // current node (>= 0 internal, < 0 leaf ~index)
+    int sp;           // LDS stack depth
+    float tcull;      // node culling distance (closest: best_t; any: light distance bound)
+    float best_t;     // float.MaxValue until the first hit (Scene.cs:45)
+    int best_rank;    // -1 none; any-hit: 1 = occluded
+    int gate_cached;  // last mesh whose exact AABB gate was evaluated
+    bool gate_ok;
+};
+
+// Starts a query.  Returns false when the ray misses the exact scene AABB
+// gate (Scene.cs:54) — the query is then complete (miss).
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool trav_begin(const rtd::SceneDev &S, const RayCtx &r, float tlimit, Trav &t,
+                                           Counts &cnt) {
+    t.node = 0;
+    t.sp = 0;
+    t.best_t = FLT_MAX;
+    t.best_rank = -1;
+    t.tcull = ANY ? tlimit : FLT_MAX;
+    t.gate_cached = -1;
+    t.gate_ok = false;
+    if (COUNT) cnt.box++;
+    return S.has_prims && rtm::ref_slab(r.o, r.inv, ld3(S.scene_lo), ld3(S.scene_hi));
+}
+
+// One traversal step: an internal node (test both children, descend, push
+// the far one) or a leaf (gate + primitive tests), then pop if needed.
+// Returns true when the query is complete.  ANY: t.best_rank = 1 iff a hit
+// with t*t < d2 exists — equivalent to the reference's closest-hit-then-
+// compare (RayTracingSetup.cs:333-345) since t >= 0 makes t -> t*t monotone.
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
+                                          int *__restrict__ st, Counts &cnt) {
+    if (t.node >= 0) {
+        const rtd::BvhNode *np = S.nodes + t.node;
+        const float4 a = np->a, b = np->b, c = np->c;
+        const int4 ch = np->d;
+        bool h0, h1;
+        float tn0, tn1;
+        test_children(a, b, c, r, t.tcull, h0, h1, tn0, tn1);
+        if (COUNT) cnt.box += 2;
+        if (h0 && h1) {
+            const bool first0 = tn0 <= tn1;
+            st[t.sp * kWaveSize] = first0 ? ch.y : ch.x;
+            ++t.sp;
+            t.node = first0 ? ch.x : ch.y;
+            return false;
+        }
+        if (h0 || h1) {
+            t.node = h0 ? ch.x : ch.y;
+            return false;
+        }
+    } else {
+        const rtd::LeafDesc L = S.leaves[~t.node];
+        bool ok = true;
+        if (L.gate >= 0) {  // the reference's per-mesh AABB gate, Scene.cs:67
+            if (L.gate != t.gate_cached) {
+                t.gate_cached = L.gate;
+                const rtd::MeshGate g = S.gates[L.gate];
+                t.gate_ok = rtm::ref_slab(r.o, r.inv, mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
+                if (COUNT) cnt.box++;
+            }
+            ok = t.gate_ok;
+        }
+        if (ok) {
+            if (L.kind == rtd::kLeafTri) {
+                for (int i = 0; i < L.count; ++i) {
+                    const rtd::TriRec tr = S.tris[L.first + i];
+                    float th;
+                    if (COUNT) cnt.tri++;
+                    if (rtm::ref_triangle(r.o, r.d, mk(tr.p0.x, tr.p0.y, tr.p0.z), mk(tr.p0.w, tr.p1.x, tr.p1.y),
+                                          mk(tr.p1.z, tr.p1.w, tr.p2.x), th)) {
+                        const int rank = __float_as_int(tr.p2.y);
+                        if (ANY) {
+                            if (th * th < d2) {
+                                t.best_rank = 1;
+                                return true;
+                            }
+                        } else if (th < t.best_t || (th == t.best_t && rank < t.best_rank)) {
+                            t.best_t = th;
+                            t.best_rank = rank;
+                            t.tcull = th;
+                        }
+                    }
+                }
+            } else {
+                for (int i = 0; i < L.count; ++i) {
+                    const rtd::SphRec sr = S.sphs[L.first + i];
+                    float th;
+                    if (COUNT) cnt.sph++;
+                    if (rtm::ref_sphere(r.o, r.d, mk(sr.cr.x, sr.cr.y, sr.cr.z), sr.cr.w, th)) {
+                        const int rank = sr.misc.x;
+                        if (ANY) {
+                            if (th * th < d2) {
+                                t.best_rank = 1;
+                                return true;
+                            }
+                        } else if (th < t.best_t || (th == t.best_t && rank < t.best_rank)) {
+                            t.best_t = th;
+                            t.best_rank = rank;
+                            t.tcull = th;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (t.sp == 0) return true;
+    --t.sp;
+    t.node = st[t.sp * kWaveSize];
+    return false;
+}
+
+// Whole query in one call (megakernel / batch-intersect path).
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool traverse(const rtd::SceneDev &S, const RayCtx &r, float tlimit, float d2,
+                                         float &best_t, int &best_rank, int *__restrict__ st, Counts &cnt) {
+    Trav t;
+    if (!trav_begin<ANY, COUNT>(S, r, tlimit, t, cnt)) {
+        best_t = FLT_MAX;
+        best_rank = -1;
+        return false;
+    }
+    while (!trav_step<ANY, COUNT>(S, r, t, d2, st, cnt)) {
+    }
+    best_t = t.best_t;
+    best_rank = t.best_rank;
+    return best_rank >= 0;
+}
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long *ctr) {
+    const unsigned p = wave_sum(c.primary), s = wave_sum(c.shadow), r = wave_sum(c.reflection);
+    unsigned b = 0, t = 0, q = 0, h = 0;
+    if (COUNT) {
+        b = wave_sum(c.box);
+        t = wave_sum(c.tri);
+        q = wave_sum(c.sph);
+        h = wave_sum(c.shading);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (p) atomicAdd(ctr + 0, (unsigned long long)p);
+        if (s) atomicAdd(ctr + 1, (unsigned long long)s);
+        if (r) atomicAdd(ctr + 2, (unsigned long long)r);
+        if (COUNT) {
+            if (b) atomicAdd(ctr + 3, (unsigned long long)b);
+            if (t) atomicAdd(ctr + 4, (unsigned long long)t);
+            if (q) atomicAdd(ctr + 5, (unsigned long long)q);
+            if (h) atomicAdd(ctr + 6, (unsigned long long)h);
+        }
+    }
+}
+
+}  // namespace rtt
