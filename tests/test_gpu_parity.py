@@ -188,3 +188,20 @@ def test_errors(gpu_ctx, rt):
         fresh.render(fr.camera, fr.plane, rt.frame_params(fr))
     assert e.value.status == rt.abi.RT_E_STATE
     fresh.close()
+
+
+def test_cpp_host_mirror_demo(tmp_path):
+    """The C++ host mirror (unity-raytracer_amd/host/RayTracer.hpp) renders the
+    reference demo scene through the C-ABI in a process without torch; its
+    PixelColors equal the committed golden frame."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "unity-raytracer_amd", "lib", "cast_pixel_rays")
+    out = tmp_path / "demo.f32"
+    r = subprocess.run([exe, str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    img = np.fromfile(out, np.float32).reshape(50, 50, 4)
+    g = np.load(os.path.join(root, "tests", "golden", "frames.npz"))
+    assert np.array_equal(img[..., :3].view(np.uint32), g["demo"].view(np.uint32))
+    assert np.all(img[..., 3] == 1.0)

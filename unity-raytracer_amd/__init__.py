@@ -4,7 +4,7 @@ vectorized-runner/unity-raytracer, behind the C-ABI in include/rt_mi355.h.
 Import with ``_rt_pkg.load()`` from the repo root (the directory name has a
 hyphen, so it is loaded under the module name ``unity_raytracer_amd``).
 """
-from . import abi, scene, scenes, raytracing  # noqa: F401
+from . import abi, bands, scene, scenes, raytracing  # noqa: F401
 from .abi import load_library, RtError  # noqa: F401
 from .scene import Scene, Mesh, MaterialData, TriangleData, SphereData  # noqa: F401
 from .scenes import CameraData, ImagePlane, Frame, make  # noqa: F401
