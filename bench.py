@@ -85,7 +85,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=["wavefront", "megakernel"], default="wavefront")
+    ap.add_argument("--mode", choices=["megakernel", "wavefront", "packet"], default="megakernel")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,7 +110,7 @@ def main():
     local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if world > 1 else ry
     out = torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda")
     nbytes = out.numel() * 4
-    mode_flags = rt.abi.RT_FLAG_MEGAKERNEL if args.mode == "megakernel" else 0
+    mode_flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET}.get(args.mode, 0)
     params = rt.frame_params(fr, band_index=rank if world > 1 else 0, band_count=band_count, band_rows=R,
                              flags=mode_flags)
     if world > 1:
@@ -193,7 +193,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": load_traffic(args.config),
-                "kernel": "render_kernel<false>" if args.mode == "megakernel" else "wavefront passes (sum)",
+                "kernel": {"megakernel": "render_kernel<false>", "packet": "render_packet_kernel<false,1>"}.get(
+                    args.mode, "wavefront passes (sum)"),
                 "bytes_per_launch": bytes_per_launch,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
             },

@@ -141,7 +141,8 @@ typedef struct rt_render_params {
 } rt_render_params;
 
 #define RT_FLAG_COUNT_TESTS 1   /* fill rt_stats box/triangle/sphere counters (slower) */
-#define RT_FLAG_MEGAKERNEL  2   /* one-launch megakernel instead of the wavefront passes */
+#define RT_FLAG_WAVEFRONT   2   /* per-level wavefront passes instead of the default megakernel */
+#define RT_FLAG_PACKET      4   /* wave-synchronous megakernel with per-wave packet traversal */
 
 /* Work counters and timings of the last render. */
 typedef struct rt_stats {

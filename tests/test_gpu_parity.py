@@ -30,7 +30,7 @@ def _check(img, ref, st, counts, name):
     assert got == want, f"{name}: ray counts {got} != oracle {want}"
 
 
-MODES = {"wavefront": 0, "megakernel": 2}  # rt_render_params.flags (RT_FLAG_MEGAKERNEL)
+MODES = {"megakernel": 0, "wavefront": 2, "packet": 4}  # rt_render_params.flags
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -53,14 +53,15 @@ def test_frame_vs_oracle(gpu_ctx, rt, orc, name, res, spp, mode):
 
 
 def test_modes_bit_identical_full_c3(gpu_ctx, rt):
-    """Wavefront and megakernel frames are bit-identical at full C3 size, and
-    so are their ray counts."""
+    """Megakernel, wavefront and packet frames are bit-identical at full C3
+    size, and so are their ray counts."""
     fr = rt.make("C3")
     a, sa = _render(gpu_ctx, rt, fr, flags=0)
-    b, sb = _render(gpu_ctx, rt, fr, flags=2)
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
-    assert (sa.primary_rays, sa.shadow_rays, sa.reflection_rays) == (sb.primary_rays, sb.shadow_rays,
-                                                                     sb.reflection_rays)
+    for flags in (2, 4):
+        b, sb = _render(gpu_ctx, rt, fr, flags=flags)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), flags
+        assert (sa.primary_rays, sa.shadow_rays, sa.reflection_rays) == (sb.primary_rays, sb.shadow_rays,
+                                                                         sb.reflection_rays), flags
 
 
 def test_goldens(gpu_ctx, rt):

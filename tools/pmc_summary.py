@@ -1,0 +1,67 @@
+"""Summarise rocprofv3 --pmc counter CSVs per kernel (mean per dispatch).
+
+    python tools/pmc_summary.py gpurun_out/pmcA gpurun_out/pmcB ... --kernel render_kernel --out profiles/pmc_C3.json
+
+HBM bytes (gfx950, MI355X_MICROARCH.md "HBM"): TCC_EA0_RDREQ_{32B,64B,128B}
+and TCC_EA0_WRREQ(_64B) count L2 -> fabric requests (Infinity-Cache hits are
+counted too, so this is an upper bound on DRAM bytes):
+  read  = 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B (if the split counters
+          are present; otherwise 2 * 64 * RDREQ, the guide's wide-read correction)
+  write = 64*WRREQ_64B + 32*(WRREQ - WRREQ_64B)
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def load(dirs):
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch]
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            per = defaultdict(lambda: defaultdict(float))
+            names = {}
+            for row in csv.DictReader(open(f)):
+                did = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                names[did] = row["Kernel_Name"]
+                per[did][row["Counter_Name"]] += float(row["Counter_Value"])
+            for did, cs in per.items():
+                for c, v in cs.items():
+                    vals[names[did]][c].append(v)
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--kernel", default="render_kernel<false>")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    vals = load(a.dirs)
+    summary = {}
+    for k, cs in vals.items():
+        summary[k] = {c: sum(v) / len(v) for c, v in cs.items()}
+    pick = {k: v for k, v in summary.items() if a.kernel in k}
+    res = {"kernels": summary}
+    if pick:
+        name, c = max(pick.items(), key=lambda kv: len(kv[1]))
+        rd = None
+        if "TCC_EA0_RDREQ_32B" in c and "TCC_EA0_RDREQ_64B" in c and "TCC_EA0_RDREQ_128B" in c:
+            rd = 32 * c["TCC_EA0_RDREQ_32B"] + 64 * c["TCC_EA0_RDREQ_64B"] + 128 * c["TCC_EA0_RDREQ_128B"]
+        elif "TCC_EA0_RDREQ" in c:
+            rd = 2 * 64 * c["TCC_EA0_RDREQ"]
+        wr = None
+        if "TCC_EA0_WRREQ" in c:
+            w64 = c.get("TCC_EA0_WRREQ_64B", 0.0)
+            wr = 64 * w64 + 32 * (c["TCC_EA0_WRREQ"] - w64)
+        res.update({"kernel": name, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                    "hbm_bytes_per_launch": (rd or 0) + (wr or 0) if rd is not None else None})
+    print(json.dumps(res, indent=1))
+    if a.out:
+        json.dump(res, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,73 @@
+"""Perf probe: time render modes of one or more library variants on a config.
+
+    python tools/probe.py --config C3 --variants default,bvh2 --frames 10
+Variants are built by `make -C unity-raytracer_amd VARIANT=name EXTRA=...`.
+Prints one JSON line per (variant, mode)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+import _rt_pkg  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--variants", default="default")
+    ap.add_argument("--modes", default="megakernel,packet,wavefront")
+    ap.add_argument("--frames", type=int, default=10)
+    ap.add_argument("--spp", type=int, default=0)
+    ap.add_argument("--res", default="")
+    ap.add_argument("--bounces", type=int, default=-99)
+    ap.add_argument("--no-lights", action="store_true")
+    a = ap.parse_args()
+    rt = _rt_pkg.load()
+    fr = rt.make(a.config)
+    if a.res:
+        fr = fr.with_resolution(*map(int, a.res.split("x")))
+    if a.spp:
+        fr = fr.with_(spp=a.spp)
+    if a.bounces != -99:
+        fr = fr.with_(max_bounces=a.bounces)
+    if a.no_lights:
+        import numpy as np
+        fr.scene.PointLights = np.zeros((0, 6), np.float32)
+    for v in a.variants.split(","):
+        path = None if v == "default" else os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", v,
+                                                         "librt_mi355.so")
+        ctx = rt.Context(lib_path=path)
+        ctx.set_scene(fr.scene)
+        out = torch.empty((fr.plane.ResolutionY, fr.plane.ResolutionX, 4), dtype=torch.float32, device="cuda")
+        ref = None
+        for mode in a.modes.split(","):
+            flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET}.get(mode, 0)
+            p = rt.frame_params(fr, flags=flags)
+            cst = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=flags | 1), out.data_ptr(),
+                                    out.numel() * 4)
+            img = out.cpu()
+            same = None if ref is None else bool(torch.equal(img.view(torch.int32), ref.view(torch.int32)))
+            ref = img if ref is None else ref
+            for _ in range(2):
+                ctx.render_device(fr.camera, fr.plane, p, out.data_ptr(), out.numel() * 4)
+            ks, ts = [], []
+            for _ in range(a.frames):
+                st = ctx.render_device(fr.camera, fr.plane, p, out.data_ptr(), out.numel() * 4)
+                ks.append(st.kernel_ms)
+                ts.append(st.total_ms)
+            rays = st.primary_rays + st.shadow_rays + st.reflection_rays
+            km = statistics.median(ks)
+            print(json.dumps({"variant": v, "mode": mode, "config": fr.name, "spp": fr.spp,
+                              "bounces": fr.max_bounces, "lights": len(fr.scene.PointLights), "kernel_ms": round(km, 4),
+                              "total_ms": round(statistics.median(ts), 4), "Mrays_s": round(rays / km / 1e3, 1),
+                              "rays": rays, "box": cst.box_tests, "tri": cst.triangle_tests,
+                              "sph": cst.sphere_tests, "same_as_first": same}), flush=True)
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -24,7 +24,8 @@ RT_E_STATE = -5
 RT_E_INTERNAL = -6
 
 RT_FLAG_COUNT_TESTS = 1
-RT_FLAG_MEGAKERNEL = 2
+RT_FLAG_WAVEFRONT = 2
+RT_FLAG_PACKET = 4
 
 STATUS_NAMES = {
     RT_OK: "RT_OK",

@@ -185,6 +185,86 @@ struct Builder {
 
 }  // namespace
 
+namespace {
+
+float box_area(const float lo[3], const float hi[3]) {
+    const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return 2.0f * (dx * dy + dy * dz + dz * dx);
+}
+
+struct Slot {
+    int ref2;  // BVH2 child ref
+    float lo[3], hi[3];
+};
+
+void child_boxes(const rtd::BvhNode &n, Slot &a, Slot &b) {
+    a.ref2 = n.d.x;
+    b.ref2 = n.d.y;
+    a.lo[0] = n.a.x; a.hi[0] = n.a.y; a.lo[1] = n.a.z; a.hi[1] = n.a.w; a.lo[2] = n.c.x; a.hi[2] = n.c.y;
+    b.lo[0] = n.b.x; b.hi[0] = n.b.y; b.lo[1] = n.b.z; b.hi[1] = n.b.w; b.lo[2] = n.c.z; b.hi[2] = n.c.w;
+}
+
+int collapse(const BuildResult &B, int node2, int depth, std::vector<rtd::BvhNode4> &out, int &max_depth) {
+    max_depth = std::max(max_depth, depth);
+    const int idx = (int)out.size();
+    out.push_back(rtd::BvhNode4{});
+    Slot slots[4];
+    int n = 2;
+    child_boxes(B.nodes[node2], slots[0], slots[1]);
+    while (n < 4) {
+        int best = -1;
+        float best_a = -1.0f;
+        for (int i = 0; i < n; ++i)
+            if (slots[i].ref2 >= 0) {
+                const float a = box_area(slots[i].lo, slots[i].hi);
+                if (a > best_a) { best_a = a; best = i; }
+            }
+        if (best < 0) break;
+        Slot a, b;
+        child_boxes(B.nodes[slots[best].ref2], a, b);
+        slots[best] = a;
+        slots[n++] = b;
+    }
+    int refs[4] = {0, 0, 0, 0};
+    float lo[3][4], hi[3][4];
+    const float inf = std::numeric_limits<float>::infinity();
+    for (int i = 0; i < 4; ++i) {
+        bool empty = i >= n;
+        if (!empty && slots[i].ref2 < 0) {
+            const rtd::LeafDesc &L = B.leaves[~slots[i].ref2];
+            if (L.count == 0) empty = true;
+            else refs[i] = rtd::encode_leaf(L.first, L.count, L.kind);
+        }
+        for (int a = 0; a < 3; ++a) {
+            lo[a][i] = empty ? inf : slots[i].lo[a];
+            hi[a][i] = empty ? inf : slots[i].hi[a];
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        if (slots[i].ref2 >= 0) refs[i] = collapse(B, slots[i].ref2, depth + 1, out, max_depth);
+    rtd::BvhNode4 &nd = out[idx];
+    nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+    nd.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+    nd.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+    nd.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+    nd.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+    nd.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    nd.child = make_int4(refs[0], refs[1], refs[2], refs[3]);
+    nd.pad = make_int4(0, 0, 0, 0);
+    return idx;
+}
+
+}  // namespace
+
+int collapse_bvh4(const BuildResult &B, std::vector<rtd::BvhNode4> &out) {
+    out.clear();
+    if (B.nodes.empty()) return 0;
+    out.reserve(B.nodes.size() / 2 + 1);
+    int max_depth = 0;
+    collapse(B, 0, 0, out, max_depth);
+    return max_depth;
+}
+
 BuildResult build_bvh(std::vector<Prim> &prims, int max_leaf) {
     auto t0 = std::chrono::steady_clock::now();
     BuildResult R;

@@ -9,7 +9,8 @@
 //     unpadded per-mesh AABB gate (Scene.cs:67) is applied per leaf;
 //   * child boxes are padded outward so the (approximate) node test never
 //     culls a primitive the exact Möller–Trumbore / sphere test accepts;
-//   * internal depth < rtd::kStackSize so the LDS stack cannot overflow.
+//   * BVH2 internal depth <= 31, so the traversal stack (kStackTotal entries,
+//     >= 3 per BVH4 level) cannot overflow.
 #pragma once
 
 #include <cstdint>
@@ -35,6 +36,10 @@ struct BuildResult {
     int max_depth = 0;
     double build_ms = 0.0;
 };
+
+// Collapse a BVH2 into 4-wide nodes (largest-area internal child expanded
+// first), leaves inlined into the child refs.  Returns the max depth.
+int collapse_bvh4(const BuildResult &B, std::vector<rtd::BvhNode4> &out);
 
 // Build over prims (reordered in place).  Always produces >= 1 internal node
 // when prims is non-empty (a lone leaf hangs off the root beside an empty child).

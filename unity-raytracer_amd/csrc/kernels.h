@@ -13,6 +13,11 @@ namespace rtk {
 hipError_t launch_render_mega(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
                               hipStream_t stream);
 
+// Packet megakernel: wave-synchronous levels, coherent rays traced one BVH
+// path per wave (packet.h).
+hipError_t launch_render_packet(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
+                                hipStream_t stream);
+
 // Wavefront: per-level queues in HBM, persistent traversal with dynamic ray
 // fetch (trace_wf.hip); chunk_tiles tiles (64 slots each) per pass sequence.
 hipError_t launch_render_wavefront(const rtd::SceneDev &S, const rtd::FrameDev &F, const rtw::Args &A,

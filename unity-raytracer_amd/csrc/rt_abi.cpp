@@ -29,7 +29,7 @@
 namespace {
 
 struct DeviceArrays {
-    void *nodes = nullptr, *leaves = nullptr, *tris = nullptr, *sphs = nullptr, *shade = nullptr,
+    void *nodes = nullptr, *nodes4 = nullptr, *leaves = nullptr, *tris = nullptr, *sphs = nullptr, *shade = nullptr,
          *mats = nullptr, *lights = nullptr, *gates = nullptr;
 };
 
@@ -87,7 +87,7 @@ int fail(rt_ctx *ctx, int status, const char *fmt, ...) {
     } while (0)
 
 void free_scene(rt_ctx *c) {
-    void **ps[] = {&c->arr.nodes, &c->arr.leaves, &c->arr.tris, &c->arr.sphs,
+    void **ps[] = {&c->arr.nodes, &c->arr.nodes4, &c->arr.leaves, &c->arr.tris, &c->arr.sphs,
                    &c->arr.shade, &c->arr.mats,   &c->arr.lights, &c->arr.gates};
     for (void **p : ps) {
         if (*p) (void)hipFree(*p);
@@ -283,25 +283,33 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, float4
     F.out = d_out;
     F.counters = ctx->d_counters;
     const bool count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
-    const bool mega = (prm->flags & RT_FLAG_MEGAKERNEL) != 0;
+    const bool packet = (prm->flags & RT_FLAG_PACKET) != 0;
+    const bool wavefront = !packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
+    const bool mega = !packet && !wavefront;  // default
     int chunk_tiles = 0;
     rtw::Args A{};
-    if (!mega && F.num_tiles > 0) {
+    if (wavefront && F.num_tiles > 0) {
         int st = prepare_wavefront(ctx, F, chunk_tiles, A);
         if (st) return st;
     }
-    HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
+    HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    if (mega)
+    if (packet)
+        HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));
+    else if (mega)
         HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, count, ctx->stream));
-    else if (F.num_tiles > 0)
+    else if (wavefront && F.num_tiles > 0)
         HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, count, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    unsigned long long counts[8] = {0};
-    HIP_OR_FAIL(ctx, hipMemcpyAsync(counts, ctx->d_counters, sizeof counts, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<unsigned long long> slots((size_t)rtd::kCounterSlots * rtd::kCounterWords);
+    HIP_OR_FAIL(ctx, hipMemcpyAsync(slots.data(), ctx->d_counters, ctr_bytes, hipMemcpyDeviceToHost, ctx->stream));
     if (host_out && out_bytes)
         HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long counts[rtd::kCounterWords] = {0};
+    for (int sl = 0; sl < rtd::kCounterSlots; ++sl)
+        for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] += slots[(size_t)sl * rtd::kCounterWords + w];
     if (stats) {
         float ms = 0.0f;
         HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -348,7 +356,8 @@ int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->d_counters, rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long)) !=
+            hipSuccess) {
         rt_destroy(c);
         return fail(nullptr, RT_E_HIP, "stream/event/counter allocation failed");
     }
@@ -514,7 +523,7 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
         p.payload = rank;
         prims.push_back(p);
         sph_src[i].cr = make_float4(s.center.x, s.center.y, s.center.z, s.radius_squared);
-        sph_src[i].misc = make_int4(rank, 0, 0, 0);
+        sph_src[i].misc = make_int4(rank, -1, 0, 0);
         const int mid = mat_id(sc->sphere_materials[i]);
         shade[rank] = make_float4(s.center.x, s.center.y, s.center.z, 0.0f);
         std::memcpy(&shade[rank].w, &mid, 4);
@@ -532,6 +541,13 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
     ctx->last_bvh_depth = B.max_depth;
     if (B.max_depth > rtd::kMaxTreeDepth)
         return fail(ctx, RT_E_INTERNAL, "BVH depth %d exceeds stack", B.max_depth);
+    std::vector<rtd::BvhNode4> nodes4;
+    const int depth4 = rtb::collapse_bvh4(B, nodes4);
+    if (3 * (depth4 + 1) > rtd::kStackTotal)
+        return fail(ctx, RT_E_INTERNAL, "BVH4 depth %d exceeds stack", depth4);
+    std::vector<int> tri_gate((size_t)P, -1);
+    for (int m = 0; m < sc->mesh_count; ++m)
+        for (int r = ctx->mesh_rank_first[m]; r < ctx->mesh_rank_first[m + 1]; ++r) tri_gate[r] = m;
 
     std::vector<rtd::TriRec> tris(B.tri_order.size());
     for (size_t i = 0; i < B.tri_order.size(); ++i) {
@@ -542,7 +558,9 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
         std::memcpy(&rbits, &rk, 4);
         tris[i].p0 = make_float4(t.v0.x, t.v0.y, t.v0.z, e1.x);
         tris[i].p1 = make_float4(e1.y, e1.z, e2.x, e2.y);
-        tris[i].p2 = make_float4(e2.z, rbits, 0.0f, 0.0f);
+        float gbits;
+        std::memcpy(&gbits, &tri_gate[rk], 4);
+        tris[i].p2 = make_float4(e2.z, rbits, gbits, 0.0f);
     }
     std::vector<rtd::SphRec> sphs(B.sph_order.size());
     for (size_t i = 0; i < B.sph_order.size(); ++i) sphs[i] = sph_src[B.sph_order[i] - MT];
@@ -560,6 +578,7 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
     }
 
     HIP_OR_FAIL(ctx, upload(&ctx->arr.nodes, B.nodes));
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.nodes4, nodes4));
     HIP_OR_FAIL(ctx, upload(&ctx->arr.leaves, B.leaves));
     HIP_OR_FAIL(ctx, upload(&ctx->arr.tris, tris));
     HIP_OR_FAIL(ctx, upload(&ctx->arr.sphs, sphs));
@@ -570,6 +589,7 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
 
     rtd::SceneDev &S = ctx->S;
     S.nodes = (const rtd::BvhNode *)ctx->arr.nodes;
+    S.nodes4 = (const rtd::BvhNode4 *)ctx->arr.nodes4;
     S.leaves = (const rtd::LeafDesc *)ctx->arr.leaves;
     S.tris = (const rtd::TriRec *)ctx->arr.tris;
     S.sphs = (const rtd::SphRec *)ctx->arr.sphs;

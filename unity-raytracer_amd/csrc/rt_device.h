@@ -25,12 +25,25 @@
 
 namespace rtd {
 
-constexpr int kStackSize = 32;      // LDS traversal stack entries per lane
-constexpr int kMaxTreeDepth = 31;   // builder guarantees internal depth < kStackSize
+#ifndef RT_STACK_LDS
+#define RT_STACK_LDS 24
+#endif
+#ifndef RT_BVH4
+#define RT_BVH4 1
+#endif
+constexpr int kStackSize = RT_STACK_LDS;  // LDS traversal stack entries per lane
+constexpr int kStackTotal = 96;           // + private (scratch) overflow; >= 3 * max BVH4 depth
+constexpr int kMaxTreeDepth = 31;         // builder guarantees BVH2 internal depth <= 31
 constexpr int kMaxBounces = 32;     // per-lane mirror fold stack
 constexpr int kWaveSize = 64;
 constexpr int kBlockThreads = 256;  // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;
+
+// Ray/test counters are sharded: slot = block % kCounterSlots, 8 x u64 (one
+// 64-B line) per slot; the host sums the slots.  One shared word would
+// serialise every wave's atomics (a single word saturates near 88 atomics/us).
+constexpr int kCounterSlots = 256;
+constexpr int kCounterWords = 8;
 
 constexpr int kLeafTri = 0;
 constexpr int kLeafSphere = 1;
@@ -42,6 +55,21 @@ struct alignas(16) BvhNode {
     int4 d;    // child0, child1 (>= 0 internal node, < 0 leaf ~index), unused
 };
 
+// 4-wide node (BVH2 collapsed, 128 B = one L2 line): the four child boxes
+// stored plane by plane so one lane tests four boxes from 6 float4 loads.
+// Child refs: >= 0 internal node; < 0 leaf, ~ref = first | (count-1) << 27 |
+// kind << 29 (first indexes tris[] or sphs[]); empty slots have +inf boxes.
+struct alignas(16) BvhNode4 {
+    float4 lox, hix, loy, hiy, loz, hiz;
+    int4 child;
+    int4 pad;
+};
+
+constexpr int kLeafFirstBits = 27;
+__host__ __device__ __forceinline__ int encode_leaf(int first, int count, int kind) {
+    return ~(first | ((count - 1) << kLeafFirstBits) | (kind << (kLeafFirstBits + 2)));
+}
+
 struct alignas(16) LeafDesc {
     int first;  // into tris[] or sphs[]
     int count;
@@ -52,12 +80,12 @@ struct alignas(16) LeafDesc {
 struct alignas(16) TriRec {
     float4 p0;  // v0.x v0.y v0.z e1.x
     float4 p1;  // e1.y e1.z e2.x e2.y
-    float4 p2;  // e2.z rank(bits) - -
+    float4 p2;  // e2.z rank(bits) gate(bits: mesh index or -1) -
 };
 
 struct alignas(16) SphRec {
     float4 cr;  // center.xyz, radius_squared
-    int4 misc;  // rank, -, -, -
+    int4 misc;  // rank, gate (-1), -, -
 };
 
 struct alignas(16) DevMaterial {
@@ -80,6 +108,7 @@ struct alignas(16) MeshGate {
 // Everything a kernel needs to read the scene.
 struct SceneDev {
     const BvhNode *nodes;
+    const BvhNode4 *nodes4;
     const LeafDesc *leaves;
     const TriRec *tris;
     const SphRec *sphs;
@@ -113,7 +142,7 @@ struct FrameDev {
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
     float4 *out;             // local_rows x res_x RGBA
-    unsigned long long *counters;  // 7 x u64, rt_stats order
+    unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
 };
 
 }  // namespace rtd

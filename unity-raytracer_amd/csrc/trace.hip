@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels.h"
+#include "packet.h"
 #include "rt_device.h"
 #include "rt_math.h"
 #include "shade.h"
@@ -31,7 +32,7 @@ namespace {
 // results are folded back to front so c0 + km0*(c1 + km1*(...)) rounds
 // exactly like the reference.
 template <bool COUNT>
-__device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, int *st, Counts &cnt) {
+__device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st, Counts &cnt) {
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
     int depth = 0;
@@ -82,7 +83,8 @@ __global__ __launch_bounds__(kBlockThreads) void render_kernel(SceneDev S, Frame
     __shared__ int stack_mem[kWavesPerBlock * kStackSize * kWaveSize];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    int *st = stack_mem + wave * kStackSize * kWaveSize + lane;
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
     const int tile = blockIdx.x * kWavesPerBlock + wave;
     if (tile >= F.num_tiles) return;  // wave-uniform
     int px, ly, gy, s;
@@ -109,11 +111,117 @@ __global__ __launch_bounds__(kBlockThreads) void render_kernel(SceneDev S, Frame
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
 
+// Wave-synchronous megakernel: the Whitted chain advances level by level for
+// the whole wave; rays of levels < PACKET_LEVELS (camera rays and their shadow
+// rays first of all) are traced as one packet per wave (packet.h), deeper
+// mirror rays per lane (traverse.h).  Same arithmetic and results as
+// render_kernel.
+template <bool COUNT, int PACKET_LEVELS>
+__global__ __launch_bounds__(kBlockThreads) void render_packet_kernel(SceneDev S, FrameDev F) {
+    __shared__ int stack_mem[kWavesPerBlock * kStackSize * kWaveSize];
+    __shared__ int wstack_mem[kWavesPerBlock * rtp::kWaveStack];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
+    int *wstack = wstack_mem + wave * rtp::kWaveStack;
+    const int tile = blockIdx.x * kWavesPerBlock + wave;
+    if (tile >= F.num_tiles) return;  // wave-uniform
+    int px, ly, gy, s;
+    const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    float fold_c[kMaxBounces][3];
+    float fold_k[kMaxBounces][3];
+    int depth = 0;
+    f3 term = mk(0.0f, 0.0f, 0.0f);
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+    bool alive = active;
+    if (active) {
+        rts::primary_ray(F, px, gy, s, o, d);
+        cnt.primary = 1;
+    }
+    for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
+        rtt::RayCtx r;
+        rtt::setup_ray(r, o, d);
+        float bt = FLT_MAX;
+        int br = -1;
+        if (level < PACKET_LEVELS) {
+            rtp::PacketLane P;
+            rtp::packet_trace<false, COUNT>(S, r, alive, 0.0f, 0.0f, P, wstack, cnt);
+            bt = P.best_t;
+            br = P.best_rank;
+        } else if (alive) {
+            rtt::traverse<false, COUNT>(S, r, 0.0f, 0.0f, bt, br, st, cnt);
+        }
+        const bool hit = alive && br >= 0;
+        if (alive && !hit) term = rtt::ld3(F.bg255);  // :310-311
+        rts::Surface sf;
+        DevMaterial m;
+        f3 col = mk(0.0f, 0.0f, 0.0f);
+        if (hit) {
+            if (COUNT) cnt.shading++;
+            sf = rts::surface(S, o, d, bt, br);
+            m = S.mats[sf.mat];
+            col = rts::ambient(S, m);
+        }
+        for (int l = 0; l < S.num_lights; ++l) {  // :327-356, wave-uniform
+            const DevLight L = S.lights[l];
+            rts::ShadowRay sr;
+            rtt::RayCtx rs;
+            sr.o = o;
+            sr.dir = d;
+            sr.d2 = 0.0f;
+            if (hit) {
+                sr = rts::shadow_ray(sf, L);
+                cnt.shadow++;
+            }
+            rtt::setup_ray(rs, sr.o, sr.dir);
+            bool occ = false;
+            if (level < PACKET_LEVELS) {
+                rtp::PacketLane Q;
+                rtp::packet_trace<true, COUNT>(S, rs, hit, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
+                occ = Q.best_rank == 1;
+            } else if (hit) {
+                float dt;
+                int dr;
+                occ = rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt);
+            }
+            if (hit && !occ) col = col + rts::light_term(S, sf, m, L, sr);
+        }
+        const bool mirror = hit && m.ka_mirror.w != 0.0f && level < F.max_bounces;  // :358
+        if (mirror) {
+            fold_c[depth][0] = col.x; fold_c[depth][1] = col.y; fold_c[depth][2] = col.z;
+            fold_k[depth][0] = m.km.x; fold_k[depth][1] = m.km.y; fold_k[depth][2] = m.km.z;
+            rts::reflect(sf, o, d);
+            ++depth;
+            cnt.reflection++;
+        } else if (hit) {
+            term = col;
+        }
+        alive = mirror;
+    }
+    for (int k = depth - 1; k >= 0; --k)
+        term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
+    const f3 color = term;
+    f3 sum = color;
+    for (int k = 1; k < F.spp; ++k) {
+        const int src = lane + k;
+        sum = sum + mk(__shfl(color.x, src), __shfl(color.y, src), __shfl(color.z, src));
+    }
+    if (active && s == 0) {
+        f3 v = sum;
+        if (F.spp > 1) v = v / (float)F.spp;
+        F.out[(size_t)ly * F.res_x + px] = make_float4(v.x / 255.0f, v.y / 255.0f, v.z / 255.0f, 1.0f);  // Rgb.cs:13
+    }
+    rtt::flush_counts<COUNT>(cnt, F.counters);
+}
+
 __global__ __launch_bounds__(kBlockThreads) void intersect_kernel(SceneDev S, const float *rays, int n, int4 *out) {
     __shared__ int stack_mem[kWavesPerBlock * kStackSize * kWaveSize];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    int *st = stack_mem + wave * kStackSize * kWaveSize + lane;
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
     const int i = blockIdx.x * kBlockThreads + threadIdx.x;
     if (i >= n) return;
     const float *rr = rays + (size_t)i * 6;
@@ -149,6 +257,22 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kBlockThreads), 0, stream, S, F);
     else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kBlockThreads), 0, stream, S, F);
+    return hipGetLastError();
+}
+
+#ifndef RT_PACKET_LEVELS
+#define RT_PACKET_LEVELS 1
+#endif
+
+hipError_t launch_render_packet(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
+    if (F.num_tiles <= 0) return hipSuccess;
+    const int blocks = (F.num_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (count_tests)
+        hipLaunchKernelGGL((render_packet_kernel<true, RT_PACKET_LEVELS>), dim3(blocks), dim3(kBlockThreads), 0,
+                           stream, S, F);
+    else
+        hipLaunchKernelGGL((render_packet_kernel<false, RT_PACKET_LEVELS>), dim3(blocks), dim3(kBlockThreads), 0,
+                           stream, S, F);
     return hipGetLastError();
 }
 

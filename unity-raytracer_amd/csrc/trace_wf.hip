@@ -53,7 +53,8 @@ __global__ __launch_bounds__(kBlockThreads) void wf_trace(SceneDev S, FrameDev F
     __shared__ int stack_mem[kWavesPerBlock * kStackSize * kWaveSize];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    int *st = stack_mem + wave * kStackSize * kWaveSize + lane;
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
     const int n_level = PRIMARY ? A.n0 : A.ctr->n[level];
     const int count = ANY ? n_level * S.num_lights : n_level;
     const int base = (ANY || PRIMARY) ? 0 : level_begin(A.ctr, level);

@@ -44,6 +44,23 @@ __device__ __forceinline__ void setup_ray(RayCtx &r, f3 o, f3 d) {
 
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
+// Load through the constant address space: with a wave-uniform address the
+// backend emits a scalar (SMEM) load — one fetch per wave into SGPRs.
+typedef const __attribute__((address_space(4))) int *const_i32_ptr;
+
+template <typename T>
+__device__ __forceinline__ T cload(const T *p) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized records only");
+    const_i32_ptr q = (const_i32_ptr)p;
+    union {
+        T v;
+        int w[sizeof(T) / 4];
+    } u;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) u.w[i] = q[i];
+    return u.v;
+}
+
 // Conservative slab test of both children of a node (padded boxes; FMA form).
 __device__ __forceinline__ void test_children(const float4 a, const float4 b, const float4 c, const RayCtx &r,
                                               float tcull, bool &h0, bool &h1, float &tn0, float &tn1) {
@@ -61,16 +78,46 @@ __device__ __forceinline__ void test_children(const float4 a, const float4 b, co
     h1 = tn1 <= tf1;
 }
 
-// Resumable traversal state of one lane.
+// Resumable traversal state of one lane.  The stack is hybrid: the first
+// kStackSize entries live in LDS (st, stride 64 lanes), deeper ones in a
+// private (scratch) array that only very deep trees ever touch.
 struct Trav {
-    int node;         // current node (>= 0 internal, < 0 leaf ~index)
-    int sp;           // LDS stack depth
+    int node;         // current node (>= 0 internal, < 0 leaf ref)
+    int sp;           // stack depth
     float tcull;      // node culling distance (closest: best_t; any: light distance bound)
     float best_t;     // float.MaxValue until the first hit (Scene.cs:45)
     int best_rank;    // -1 none; any-hit: 1 = occluded
     int gate_cached;  // last mesh whose exact AABB gate was evaluated
     bool gate_ok;
 };
+
+// Lane stack: LDS part (stride 64 lanes) + private overflow.  The overflow is
+// accessed through a volatile pointer so the compiler can never fold the two
+// loads into one generic (flat) load, and it lives outside Trav so the
+// traversal state stays in registers.
+struct Stack {
+    int *lds;
+    int *ovf;
+};
+
+__device__ __forceinline__ void push(Trav &t, const Stack &st, int v) {
+    if (t.sp < rtd::kStackSize)
+        st.lds[t.sp * kWaveSize] = v;
+    else
+        ((volatile int *)st.ovf)[t.sp - rtd::kStackSize] = v;
+    ++t.sp;
+}
+
+// false when the stack is empty
+__device__ __forceinline__ bool pop(Trav &t, const Stack &st) {
+    if (t.sp == 0) return false;
+    --t.sp;
+    if (t.sp < rtd::kStackSize)
+        t.node = st.lds[t.sp * kWaveSize];
+    else
+        t.node = ((volatile int *)st.ovf)[t.sp - rtd::kStackSize];
+    return true;
+}
 
 // Starts a query.  Returns false when the ray misses the exact scene AABB
 // gate (Scene.cs:54) — the query is then complete (miss).
@@ -88,15 +135,118 @@ __device__ __forceinline__ bool trav_begin(const rtd::SceneDev &S, const RayCtx 
     return S.has_prims && rtm::ref_slab(r.o, r.inv, ld3(S.scene_lo), ld3(S.scene_hi));
 }
 
-// One traversal step: an internal node (test both children, descend, push
-// the far one) or a leaf (gate + primitive tests), then pop if needed.
+// Primitive tests of one leaf (first, count, kind) behind the reference's
+// per-mesh AABB gate (Scene.cs:67).  ANY: returns true on an occluder.
+template <bool ANY, bool COUNT, bool UNIFORM = false>
+__device__ __forceinline__ bool leaf(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2, int first,
+                                     int count, int kind, int gate, Counts &cnt) {
+    if (gate >= 0) {
+        if (gate != t.gate_cached) {
+            t.gate_cached = gate;
+            const rtd::MeshGate g = S.gates[gate];
+            t.gate_ok = rtm::ref_slab(r.o, r.inv, mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
+            if (COUNT) cnt.box++;
+        }
+        if (!t.gate_ok) return false;
+    }
+    if (kind == rtd::kLeafTri) {
+        for (int i = 0; i < count; ++i) {
+            const rtd::TriRec tr = UNIFORM ? cload(S.tris + first + i) : S.tris[first + i];
+            float th;
+            if (COUNT) cnt.tri++;
+            if (rtm::ref_triangle(r.o, r.d, mk(tr.p0.x, tr.p0.y, tr.p0.z), mk(tr.p0.w, tr.p1.x, tr.p1.y),
+                                  mk(tr.p1.z, tr.p1.w, tr.p2.x), th)) {
+                const int rank = __float_as_int(tr.p2.y);
+                if (ANY) {
+                    if (th * th < d2) {
+                        t.best_rank = 1;
+                        return true;
+                    }
+                } else if (th < t.best_t || (th == t.best_t && rank < t.best_rank)) {
+                    t.best_t = th;
+                    t.best_rank = rank;
+                    t.tcull = th;
+                }
+            }
+        }
+    } else {
+        for (int i = 0; i < count; ++i) {
+            const rtd::SphRec sr = UNIFORM ? cload(S.sphs + first + i) : S.sphs[first + i];
+            float th;
+            if (COUNT) cnt.sph++;
+            if (rtm::ref_sphere(r.o, r.d, mk(sr.cr.x, sr.cr.y, sr.cr.z), sr.cr.w, th)) {
+                const int rank = sr.misc.x;
+                if (ANY) {
+                    if (th * th < d2) {
+                        t.best_rank = 1;
+                        return true;
+                    }
+                } else if (th < t.best_t || (th == t.best_t && rank < t.best_rank)) {
+                    t.best_t = th;
+                    t.best_rank = rank;
+                    t.tcull = th;
+                }
+            }
+        }
+    }
+    return false;
+}
+
+// Conservative slab test of one child of a 4-wide node: its entry distance,
+// or +inf when culled.
+__device__ __forceinline__ float child_key(float lx, float hx, float ly, float hy, float lz, float hz,
+                                           const RayCtx &r, float tcull) {
+    const float ax = fmaf(lx, r.ninv.x, -r.noi.x), bx = fmaf(hx, r.ninv.x, -r.noi.x);
+    const float ay = fmaf(ly, r.ninv.y, -r.noi.y), by = fmaf(hy, r.ninv.y, -r.noi.y);
+    const float az = fmaf(lz, r.ninv.z, -r.noi.z), bz = fmaf(hz, r.ninv.z, -r.noi.z);
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tcull));
+    return tn <= tf ? tn : INFINITY;
+}
+
+#define RT_CSWAP(i, j)                          \
+    do {                                        \
+        const bool sw_ = k##j < k##i;           \
+        const float tk_ = sw_ ? k##j : k##i;    \
+        k##j = sw_ ? k##i : k##j;               \
+        k##i = tk_;                             \
+        const int tr_ = sw_ ? c##j : c##i;      \
+        c##j = sw_ ? c##i : c##j;               \
+        c##i = tr_;                             \
+    } while (0)
+
+// One traversal step: an internal node (test its children, descend into the
+// nearest, push the others far-first) or a leaf, then pop if needed.
 // Returns true when the query is complete.  ANY: t.best_rank = 1 iff a hit
 // with t*t < d2 exists — equivalent to the reference's closest-hit-then-
 // compare (RayTracingSetup.cs:333-345) since t >= 0 makes t -> t*t monotone.
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
-                                          int *__restrict__ st, Counts &cnt) {
+                                          const Stack &st, Counts &cnt) {
     if (t.node >= 0) {
+#if RT_BVH4
+        const rtd::BvhNode4 *np = S.nodes4 + t.node;
+        const float4 lx = np->lox, hx = np->hix, ly = np->loy, hy = np->hiy, lz = np->loz, hz = np->hiz;
+        const int4 ch = np->child;
+        float k0 = child_key(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, t.tcull);
+        float k1 = child_key(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, t.tcull);
+        float k2 = child_key(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, t.tcull);
+        float k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, t.tcull);
+        if (COUNT) cnt.box += 4;
+        int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+        RT_CSWAP(0, 1);
+        RT_CSWAP(2, 3);
+        RT_CSWAP(0, 2);
+        RT_CSWAP(1, 3);
+        RT_CSWAP(1, 2);
+        if (k0 != INFINITY) {
+            if (k3 != INFINITY) push(t, st, c3);
+            if (k2 != INFINITY) push(t, st, c2);
+            if (k1 != INFINITY) push(t, st, c1);
+            t.node = c0;
+            return false;
+        }
+#else
         const rtd::BvhNode *np = S.nodes + t.node;
         const float4 a = np->a, b = np->b, c = np->c;
         const int4 ch = np->d;
@@ -106,8 +256,7 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         if (COUNT) cnt.box += 2;
         if (h0 && h1) {
             const bool first0 = tn0 <= tn1;
-            st[t.sp * kWaveSize] = first0 ? ch.y : ch.x;
-            ++t.sp;
+            push(t, st, first0 ? ch.y : ch.x);
             t.node = first0 ? ch.x : ch.y;
             return false;
         }
@@ -115,71 +264,29 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
             t.node = h0 ? ch.x : ch.y;
             return false;
         }
+#endif
     } else {
+#if RT_BVH4
+        const int v = ~t.node;
+        const int first = v & ((1 << rtd::kLeafFirstBits) - 1);
+        const int count = ((v >> rtd::kLeafFirstBits) & 3) + 1;
+        const int kind = (v >> (rtd::kLeafFirstBits + 2)) & 1;
+        const int gate = kind == rtd::kLeafTri ? __float_as_int(S.tris[first].p2.z) : S.sphs[first].misc.y;
+#else
         const rtd::LeafDesc L = S.leaves[~t.node];
-        bool ok = true;
-        if (L.gate >= 0) {  // the reference's per-mesh AABB gate, Scene.cs:67
-            if (L.gate != t.gate_cached) {
-                t.gate_cached = L.gate;
-                const rtd::MeshGate g = S.gates[L.gate];
-                t.gate_ok = rtm::ref_slab(r.o, r.inv, mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
-                if (COUNT) cnt.box++;
-            }
-            ok = t.gate_ok;
-        }
-        if (ok) {
-            if (L.kind == rtd::kLeafTri) {
-                for (int i = 0; i < L.count; ++i) {
-                    const rtd::TriRec tr = S.tris[L.first + i];
-                    float th;
-                    if (COUNT) cnt.tri++;
-                    if (rtm::ref_triangle(r.o, r.d, mk(tr.p0.x, tr.p0.y, tr.p0.z), mk(tr.p0.w, tr.p1.x, tr.p1.y),
-                                          mk(tr.p1.z, tr.p1.w, tr.p2.x), th)) {
-                        const int rank = __float_as_int(tr.p2.y);
-                        if (ANY) {
-                            if (th * th < d2) {
-                                t.best_rank = 1;
-                                return true;
-                            }
-                        } else if (th < t.best_t || (th == t.best_t && rank < t.best_rank)) {
-                            t.best_t = th;
-                            t.best_rank = rank;
-                            t.tcull = th;
-                        }
-                    }
-                }
-            } else {
-                for (int i = 0; i < L.count; ++i) {
-                    const rtd::SphRec sr = S.sphs[L.first + i];
-                    float th;
-                    if (COUNT) cnt.sph++;
-                    if (rtm::ref_sphere(r.o, r.d, mk(sr.cr.x, sr.cr.y, sr.cr.z), sr.cr.w, th)) {
-                        const int rank = sr.misc.x;
-                        if (ANY) {
-                            if (th * th < d2) {
-                                t.best_rank = 1;
-                                return true;
-                            }
-                        } else if (th < t.best_t || (th == t.best_t && rank < t.best_rank)) {
-                            t.best_t = th;
-                            t.best_rank = rank;
-                            t.tcull = th;
-                        }
-                    }
-                }
-            }
-        }
+        const int first = L.first, count = L.count, kind = L.kind, gate = L.gate;
+#endif
+        if (leaf<ANY, COUNT>(S, r, t, d2, first, count, kind, gate, cnt)) return true;
     }
-    if (t.sp == 0) return true;
-    --t.sp;
-    t.node = st[t.sp * kWaveSize];
-    return false;
+    return !pop(t, st);
 }
+
+#undef RT_CSWAP
 
 // Whole query in one call (megakernel / batch-intersect path).
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool traverse(const rtd::SceneDev &S, const RayCtx &r, float tlimit, float d2,
-                                         float &best_t, int &best_rank, int *__restrict__ st, Counts &cnt) {
+                                         float &best_t, int &best_rank, const Stack &st, Counts &cnt) {
     Trav t;
     if (!trav_begin<ANY, COUNT>(S, r, tlimit, t, cnt)) {
         best_t = FLT_MAX;
@@ -199,7 +306,8 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long *ctr) {
+__device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long *counters) {
+    unsigned long long *ctr = counters + (size_t)(blockIdx.x % rtd::kCounterSlots) * rtd::kCounterWords;
     const unsigned p = wave_sum(c.primary), s = wave_sum(c.shadow), r = wave_sum(c.reflection);
     unsigned b = 0, t = 0, q = 0, h = 0;
     if (COUNT) {
