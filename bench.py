@@ -85,7 +85,11 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="N>1: check the assembled frame against 1 rank")
     ap.add_argument("--mode", choices=["megakernel", "wavefront", "packet"], default="megakernel")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU, "
+                         "gather through host memory)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,10 +97,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local_rank)
+    gloo = args.dist_backend == "gloo"
+    ndev = torch.cuda.device_count()
+    device = local_rank % ndev if gloo else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if gloo:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", device))
 
     rt = _rt_pkg.load()
     fr = rt.make(args.config)
@@ -116,13 +126,26 @@ def main():
     if world > 1:
         gathered = torch.empty((world, local_rows, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
         image = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+        if gloo:  # host staging buffers for the rehearsal backend
+            out_h = torch.empty((local_rows, rx, 4), dtype=torch.float32)
+            gathered_h = torch.empty((world, local_rows, rx, 4), dtype=torch.float32) if rank == 0 else None
+
+    def gather_shards():
+        """Shards -> rank 0 (RCCL gather over xGMI), then the HIP reassembly kernel."""
+        if gloo:
+            out_h.copy_(out)
+            dist.gather(out_h, list(gathered_h.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                gathered.copy_(gathered_h)
+        else:
+            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            ctx.assemble_bands(gathered.data_ptr(), rx, ry, world, R, image.data_ptr())
 
     def step():
         st = ctx.render_device(fr.camera, fr.plane, params, out.data_ptr(), nbytes)
         if world > 1:
-            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                ctx.assemble_bands(gathered.data_ptr(), rx, ry, world, R, image.data_ptr())
+            gather_shards()
         return st
 
     # counting launch (untimed): algorithmic work of this rank's frame
@@ -148,8 +171,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    if world > 1 and args.verify:
+        # the assembled frame must be bit-identical to a single-rank frame
+        full = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda")
+        if rank == 0:
+            ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=mode_flags), full.data_ptr(),
+                              full.numel() * 4)
+            same = bool(torch.equal(full.view(torch.int32), image.view(torch.int32)))
+            print(json.dumps({"verify_sharded_equals_single": same}), file=sys.stderr, flush=True)
+            if not same:
+                raise SystemExit("sharded frame differs from the single-rank frame")
     if world > 1:
-        t = torch.tensor([elapsed, float(rays), kernel_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, float(rays), kernel_ms], dtype=torch.float64,
+                         device="cpu" if gloo else "cuda")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -182,7 +216,8 @@ def main():
                 "spp": fr.spp,
                 "depth": fr.max_bounces,
                 "triangles": fr.scene.triangle_count,
-                "parallelism": f"row-bands x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": f"row-bands x{world}" + ((" + gloo gather (rehearsal)" if gloo else " + RCCL gather")
+                                                        if world > 1 else ""),
                 "rays_per_frame": rays // args.steps,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
             },

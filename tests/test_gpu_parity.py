@@ -76,18 +76,22 @@ def test_goldens(gpu_ctx, rt):
         assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == tuple(g[name + "_counts"])
 
 
-def test_full_size_c3_sampled_pixels(gpu_ctx, rt, orc):
-    """BASELINE config C3 at full size (1920x1080, 4 spp, depth 8): the GPU
-    frame against the oracle on 400 seeded pixels (pixels are independent,
-    RayTracingSetup.cs:288-301)."""
-    fr = rt.make("C3")
+@pytest.mark.parametrize("name,npix", [("C2", 2000), ("C3", 400), ("C4", 150), ("C5", 120)])
+def test_full_size_sampled_pixels(gpu_ctx, rt, orc, name, npix):
+    """BASELINE configs at full size (C2/C3 1080p 4 spp depth 8, C4 4K 16 spp
+    depth 8, C5 1080p 64 spp depth 16): the GPU frame against the oracle on
+    seeded pixels (pixels are independent, RayTracingSetup.cs:288-301), plus
+    the full-frame primary ray count."""
+    fr = rt.make(name)
     img, st = _render(gpu_ctx, rt, fr)
     rng = np.random.default_rng(7)
-    idx = rng.choice(fr.plane.ResolutionX * fr.plane.ResolutionY, 400, replace=False).astype(np.int32)
+    W, H = fr.plane.ResolutionX, fr.plane.ResolutionY
+    idx = rng.choice(W * H, npix, replace=False).astype(np.int32)
     ref, _ = orc.render_pixels(fr, idx)
     got = img.reshape(-1, 4)[idx]
     assert float(np.max(np.abs(got - ref))) <= TOL
-    assert st.primary_rays == 1920 * 1080 * 4
+    assert st.primary_rays == W * H * fr.spp
+    assert np.isfinite(img).all()
 
 
 def test_intersect_rays_exact(gpu_ctx, rt, orc):

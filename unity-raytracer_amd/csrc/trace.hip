@@ -48,19 +48,22 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         }
         if (COUNT) cnt.shading++;
         const rts::Surface sf = rts::surface(S, o, d, bt, br);
-        const DevMaterial m = S.mats[sf.mat];
-        f3 col = rts::ambient(S, m);
+        f3 col = rts::ambient(S, S.mats[sf.mat]);
         for (int l = 0; l < S.num_lights; ++l) {  // :327-356
-            const DevLight L = S.lights[l];
-            const rts::ShadowRay sr = rts::shadow_ray(sf, L);
+            const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
             cnt.shadow++;
             rtt::RayCtx rs;
             rtt::setup_ray(rs, sr.o, sr.dir);
             float dt;
             int dr;
             if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) continue;
-            col = col + rts::light_term(S, sf, m, L, sr);
+#if RT_RELOAD
+            // keep material/light out of registers across the traversal
+            asm volatile("" ::: "memory");
+#endif
+            col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
         }
+        const DevMaterial m = S.mats[sf.mat];
         if (m.ka_mirror.w != 0.0f && depth < F.max_bounces) {  // :358-363
             fold_c[depth][0] = col.x; fold_c[depth][1] = col.y; fold_c[depth][2] = col.z;
             fold_k[depth][0] = m.km.x; fold_k[depth][1] = m.km.y; fold_k[depth][2] = m.km.z;
@@ -78,8 +81,12 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     return term;
 }
 
+#ifndef RT_MK_MIN_WAVES
+#define RT_MK_MIN_WAVES 4
+#endif
+
 template <bool COUNT>
-__global__ __launch_bounds__(kBlockThreads) void render_kernel(SceneDev S, FrameDev F) {
+__global__ __launch_bounds__(kBlockThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kWavesPerBlock * kStackSize * kWaveSize];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;

@@ -204,6 +204,13 @@ __device__ __forceinline__ float child_key(float lx, float hx, float ly, float h
     return tn <= tf ? tn : INFINITY;
 }
 
+#ifndef RT_ANY_NOSORT
+#define RT_ANY_NOSORT 0
+#endif
+#ifndef RT_RELOAD
+#define RT_RELOAD 0
+#endif
+
 #define RT_CSWAP(i, j)                          \
     do {                                        \
         const bool sw_ = k##j < k##i;           \
@@ -234,15 +241,36 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         float k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, t.tcull);
         if (COUNT) cnt.box += 4;
         int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-        RT_CSWAP(0, 1);
-        RT_CSWAP(2, 3);
-        RT_CSWAP(0, 2);
-        RT_CSWAP(1, 3);
-        RT_CSWAP(1, 2);
+        if (!ANY || !RT_ANY_NOSORT) {  // any-hit queries need no near-first order
+            RT_CSWAP(0, 1);
+            RT_CSWAP(2, 3);
+            RT_CSWAP(0, 2);
+            RT_CSWAP(1, 3);
+            RT_CSWAP(1, 2);
+        } else {
+            // compact the hit children to the front (order irrelevant)
+            RT_CSWAP(0, 1);
+            RT_CSWAP(2, 3);
+            RT_CSWAP(0, 2);
+            RT_CSWAP(1, 3);
+        }
         if (k0 != INFINITY) {
-            if (k3 != INFINITY) push(t, st, c3);
-            if (k2 != INFINITY) push(t, st, c2);
-            if (k1 != INFINITY) push(t, st, c1);
+            // push the other hit children far-first: bottom..top = c_{h-1} .. c1
+            const int h = 1 + (k1 != INFINITY) + (k2 != INFINITY) + (k3 != INFINITY);
+            if (t.sp + 3 <= rtd::kStackSize) {
+                // branch-free: three unconditional LDS writes, sp advances by h-1
+                const int s0 = h == 4 ? c3 : (h == 3 ? c2 : c1);
+                const int s1 = h == 4 ? c2 : c1;
+                int *p = st.lds + t.sp * kWaveSize;
+                p[0] = s0;
+                p[kWaveSize] = s1;
+                p[2 * kWaveSize] = c1;
+                t.sp += h - 1;
+            } else {
+                if (h >= 4) push(t, st, c3);
+                if (h >= 3) push(t, st, c2);
+                if (h >= 2) push(t, st, c1);
+            }
             t.node = c0;
             return false;
         }
