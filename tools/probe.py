@@ -37,6 +37,7 @@ def main():
     if a.no_lights:
         import numpy as np
         fr.scene.PointLights = np.zeros((0, 6), np.float32)
+    base_img = None
     for v in a.variants.split(","):
         path = None if v == "default" else os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", v,
                                                          "librt_mi355.so")
@@ -52,6 +53,8 @@ def main():
             img = out.cpu()
             same = None if ref is None else bool(torch.equal(img.view(torch.int32), ref.view(torch.int32)))
             ref = img if ref is None else ref
+            base_img = img if base_img is None else base_img
+            same_base = bool(torch.equal(img.view(torch.int32), base_img.view(torch.int32)))
             for _ in range(2):
                 ctx.render_device(fr.camera, fr.plane, p, out.data_ptr(), out.numel() * 4)
             ks, ts = [], []
@@ -65,7 +68,8 @@ def main():
                               "bounces": fr.max_bounces, "lights": len(fr.scene.PointLights), "kernel_ms": round(km, 4),
                               "total_ms": round(statistics.median(ts), 4), "Mrays_s": round(rays / km / 1e3, 1),
                               "rays": rays, "box": cst.box_tests, "tri": cst.triangle_tests,
-                              "sph": cst.sphere_tests, "same_as_first": same}), flush=True)
+                              "sph": cst.sphere_tests, "same_as_first": same,
+                              "same_as_base": same_base}), flush=True)
         ctx.close()
 
 

@@ -192,13 +192,26 @@ __device__ __forceinline__ bool leaf(const rtd::SceneDev &S, const RayCtx &r, Tr
     return false;
 }
 
+#ifndef RT_PK_FMA
+#define RT_PK_FMA 0
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 // Conservative slab test of one child of a 4-wide node: its entry distance,
 // or +inf when culled.
 __device__ __forceinline__ float child_key(float lx, float hx, float ly, float hy, float lz, float hz,
                                            const RayCtx &r, float tcull) {
+#if RT_PK_FMA
+    // packed FMA: both planes of an axis in one v_pk_fma_f32
+    const f2v px = __builtin_elementwise_fma((f2v){lx, hx}, (f2v){r.ninv.x, r.ninv.x}, (f2v){-r.noi.x, -r.noi.x});
+    const f2v py = __builtin_elementwise_fma((f2v){ly, hy}, (f2v){r.ninv.y, r.ninv.y}, (f2v){-r.noi.y, -r.noi.y});
+    const f2v pz = __builtin_elementwise_fma((f2v){lz, hz}, (f2v){r.ninv.z, r.ninv.z}, (f2v){-r.noi.z, -r.noi.z});
+    const float ax = px.x, bx = px.y, ay = py.x, by = py.y, az = pz.x, bz = pz.y;
+#else
     const float ax = fmaf(lx, r.ninv.x, -r.noi.x), bx = fmaf(hx, r.ninv.x, -r.noi.x);
     const float ay = fmaf(ly, r.ninv.y, -r.noi.y), by = fmaf(hy, r.ninv.y, -r.noi.y);
     const float az = fmaf(lz, r.ninv.z, -r.noi.z), bz = fmaf(hz, r.ninv.z, -r.noi.z);
+#endif
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tcull));
     return tn <= tf ? tn : INFINITY;
@@ -209,6 +222,9 @@ __device__ __forceinline__ float child_key(float lx, float hx, float ly, float h
 #endif
 #ifndef RT_RELOAD
 #define RT_RELOAD 0
+#endif
+#ifndef RT_NEAR_ONLY
+#define RT_NEAR_ONLY 0
 #endif
 
 #define RT_CSWAP(i, j)                          \
@@ -241,7 +257,16 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         float k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, t.tcull);
         if (COUNT) cnt.box += 4;
         int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-        if (!ANY || !RT_ANY_NOSORT) {  // any-hit queries need no near-first order
+        if (RT_NEAR_ONLY) {
+            // nearest child first, the others in slot order (3 compare-swaps)
+            RT_CSWAP(0, 1);
+            RT_CSWAP(0, 2);
+            RT_CSWAP(0, 3);
+            // hit children must precede misses for the push count below
+            RT_CSWAP(2, 3);
+            RT_CSWAP(1, 2);
+            RT_CSWAP(2, 3);
+        } else if (!ANY || !RT_ANY_NOSORT) {  // any-hit queries need no near-first order
             RT_CSWAP(0, 1);
             RT_CSWAP(2, 3);
             RT_CSWAP(0, 2);
