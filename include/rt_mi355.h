@@ -198,6 +198,29 @@ int rt_set_stream(rt_ctx *ctx, void *hip_stream);
  * RayTracingSetup.UpdateScene()'s result (:120-128). */
 int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *scene);
 
+/* BVH builders for rt_set_scene_ex. */
+#define RT_BUILD_SAH_HOST 0   /* binned SAH on the host, collapsed to 4-wide nodes (fastest traversal) */
+#define RT_BUILD_LBVH_GPU 1   /* linear BVH built on the GPU (Morton + radix sort + Karras), collapsed
+                                 to 4-wide nodes on the GPU: for per-frame scene rebuilds
+                                 (RayTracingSetup.cs:120-128) */
+#define RT_BUILD_LBVH_GPU_BVH2 2  /* the same tree left 2-wide (comparison / diagnostics) */
+
+/* rt_set_scene with a choice of BVH builder.  Results are identical for every
+ * builder (the BVH only accelerates Scene.IntersectRay). */
+int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *scene, int32_t build);
+
+/* What the last rt_set_scene(_ex) built. */
+typedef struct rt_scene_info {
+    int32_t build;       /* RT_BUILD_* */
+    int32_t bvh_width;   /* 4 or 2 (0: empty scene) */
+    int32_t nodes;
+    int32_t primitives;
+    double build_ms;     /* device time of the GPU build (RT_BUILD_LBVH_GPU), else 0 */
+    double total_ms;     /* wall time of the whole rt_set_scene(_ex) call */
+} rt_scene_info;
+
+int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info);
+
 /* Render one frame: the MI355X replacement of CastPixelRays (:275-302).
  * out_rgba is a caller-owned HOST buffer of resolution_x*resolution_y*4
  * floats (row-major, y = 0 is the top row, alpha = 1), i.e. PixelColors.

@@ -22,7 +22,8 @@ def _declared_functions():
 def test_header_declares_expected_entry_points():
     names = _declared_functions()
     for n in ("rt_create", "rt_destroy", "rt_set_scene", "rt_render", "rt_render_device",
-              "rt_last_error", "rt_intersect_rays", "rt_assemble_bands", "rt_abi_version"):
+              "rt_last_error", "rt_intersect_rays", "rt_assemble_bands", "rt_abi_version",
+              "rt_set_scene_ex", "rt_get_scene_info"):
         assert n in names
 
 
@@ -43,7 +44,7 @@ def test_ctypes_layouts(rt):
     a = rt.abi
     sizes = {
         a.rt_float3: 12, a.rt_triangle: 36, a.rt_sphere: 16, a.rt_aabb: 24, a.rt_material: 56,
-        a.rt_point_light: 24, a.rt_camera: 48, a.rt_image_plane: 20, a.rt_mesh: 88, a.rt_hit: 16,
+        a.rt_point_light: 24, a.rt_camera: 48, a.rt_scene_info: 32, a.rt_image_plane: 20, a.rt_mesh: 88, a.rt_hit: 16,
         a.rt_ray: 24, a.rt_render_params: 40, a.rt_stats: 72,
     }
     for t, s in sizes.items():

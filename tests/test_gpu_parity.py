@@ -13,8 +13,8 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4  # per RGB channel, Color units (Rgb.Color = Value / 255)
 
 
-def _render(ctx, rt, fr, **kw):
-    ctx.set_scene(fr.scene)
+def _render(ctx, rt, fr, build=0, **kw):
+    ctx.set_scene(fr.scene, build)
     img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
     return img, st
 
@@ -30,7 +30,9 @@ def _check(img, ref, st, counts, name):
     assert got == want, f"{name}: ray counts {got} != oracle {want}"
 
 
-MODES = {"megakernel": 0, "wavefront": 2, "packet": 4}  # rt_render_params.flags
+# name -> (rt_render_params.flags, BVH builder: 0 host SAH, 1 GPU LBVH 4-wide, 2 GPU LBVH 2-wide)
+MODES = {"megakernel": (0, 0), "wavefront": (2, 0), "packet": (4, 0), "lbvh": (0, 1), "lbvh_wavefront": (2, 1),
+         "lbvh_packet": (4, 1), "lbvh2": (0, 2)}
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -47,7 +49,8 @@ def test_frame_vs_oracle(gpu_ctx, rt, orc, name, res, spp, mode):
     if res:
         fr = fr.with_resolution(*res)
     fr = fr.with_(spp=spp)
-    img, st = _render(gpu_ctx, rt, fr, flags=MODES[mode])
+    flags, build = MODES[mode]
+    img, st = _render(gpu_ctx, rt, fr, build=build, flags=flags)
     ref, counts = orc.render(fr)
     _check(img, ref, st, counts, f"{name}/{mode}")
 

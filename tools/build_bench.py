@@ -1,0 +1,48 @@
+"""Scene build cost per builder: rt_set_scene_ex wall time (upload + build),
+GPU build kernel time (LBVH), and the frame time each BVH gives.
+
+  python tools/build_bench.py --configs C2 C3 C5 --reps 5
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import _rt_pkg  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", nargs="+", default=["C2", "C3", "C5"])
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.init()
+    rt = _rt_pkg.load()
+    ctx = rt.Context()
+    for name in a.configs:
+        fr = rt.make(name)
+        for build, label in ((0, "sah_host_bvh4"), (1, "lbvh_gpu_bvh4"), (2, "lbvh_gpu_bvh2")):
+            ctx.set_scene(fr.scene, build)  # warm (allocations, code objects)
+            infos = []
+            for _ in range(a.reps):
+                ctx.set_scene(fr.scene, build)
+                infos.append(ctx.scene_info())
+            times = []
+            for _ in range(a.frames):
+                _, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+                times.append(st.kernel_ms)
+            rec = {"config": name, "build": label, "primitives": infos[-1]["primitives"],
+                   "nodes": infos[-1]["nodes"],
+                   "set_scene_ms_min": min(i["total_ms"] for i in infos),
+                   "gpu_build_ms_min": min(i["build_ms"] for i in infos),
+                   "frame_ms_min": min(times)}
+            print(json.dumps(rec), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

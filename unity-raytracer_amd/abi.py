@@ -26,6 +26,9 @@ RT_E_INTERNAL = -6
 RT_FLAG_COUNT_TESTS = 1
 RT_FLAG_WAVEFRONT = 2
 RT_FLAG_PACKET = 4
+RT_BUILD_SAH_HOST = 0
+RT_BUILD_LBVH_GPU = 1
+RT_BUILD_LBVH_GPU_BVH2 = 2
 
 STATUS_NAMES = {
     RT_OK: "RT_OK",
@@ -141,6 +144,20 @@ class rt_stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class rt_scene_info(C.Structure):
+    _fields_ = [
+        ("build", C.c_int32),
+        ("bvh_width", C.c_int32),
+        ("nodes", C.c_int32),
+        ("primitives", C.c_int32),
+        ("build_ms", C.c_double),
+        ("total_ms", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 class rt_hit(C.Structure):
     _fields_ = [("type", C.c_int32), ("index", C.c_int32), ("mesh_index", C.c_int32), ("distance", C.c_float)]
 
@@ -158,6 +175,8 @@ SIGNATURES = {
     "rt_last_error": (C.c_char_p, [_P]),
     "rt_set_stream": (C.c_int, [_P, _P]),
     "rt_set_scene": (C.c_int, [_P, C.POINTER(rt_scene_desc)]),
+    "rt_set_scene_ex": (C.c_int, [_P, C.POINTER(rt_scene_desc), C.c_int32]),
+    "rt_get_scene_info": (C.c_int, [_P, C.POINTER(rt_scene_info)]),
     "rt_render": (C.c_int, [_P, C.POINTER(rt_camera), C.POINTER(rt_image_plane),
                             C.POINTER(rt_render_params), _P, C.POINTER(rt_stats)]),
     "rt_render_device": (C.c_int, [_P, C.POINTER(rt_camera), C.POINTER(rt_image_plane),

@@ -204,7 +204,8 @@ void child_boxes(const rtd::BvhNode &n, Slot &a, Slot &b) {
     b.lo[0] = n.b.x; b.hi[0] = n.b.y; b.lo[1] = n.b.z; b.hi[1] = n.b.w; b.lo[2] = n.c.z; b.hi[2] = n.c.w;
 }
 
-int collapse(const BuildResult &B, int node2, int depth, std::vector<rtd::BvhNode4> &out, int &max_depth) {
+int collapse(const BuildResult &B, int node2, int depth, std::vector<rtd::BvhNode4> &out, int &max_depth,
+             int empty_ref) {
     max_depth = std::max(max_depth, depth);
     const int idx = (int)out.size();
     out.push_back(rtd::BvhNode4{});
@@ -225,7 +226,7 @@ int collapse(const BuildResult &B, int node2, int depth, std::vector<rtd::BvhNod
         slots[best] = a;
         slots[n++] = b;
     }
-    int refs[4] = {0, 0, 0, 0};
+    int refs[4] = {empty_ref, empty_ref, empty_ref, empty_ref};
     float lo[3][4], hi[3][4];
     const float inf = std::numeric_limits<float>::infinity();
     for (int i = 0; i < 4; ++i) {
@@ -241,7 +242,7 @@ int collapse(const BuildResult &B, int node2, int depth, std::vector<rtd::BvhNod
         }
     }
     for (int i = 0; i < n; ++i)
-        if (slots[i].ref2 >= 0) refs[i] = collapse(B, slots[i].ref2, depth + 1, out, max_depth);
+        if (slots[i].ref2 >= 0) refs[i] = collapse(B, slots[i].ref2, depth + 1, out, max_depth, empty_ref);
     rtd::BvhNode4 &nd = out[idx];
     nd.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
     nd.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
@@ -256,12 +257,12 @@ int collapse(const BuildResult &B, int node2, int depth, std::vector<rtd::BvhNod
 
 }  // namespace
 
-int collapse_bvh4(const BuildResult &B, std::vector<rtd::BvhNode4> &out) {
+int collapse_bvh4(const BuildResult &B, std::vector<rtd::BvhNode4> &out, int empty_ref) {
     out.clear();
     if (B.nodes.empty()) return 0;
     out.reserve(B.nodes.size() / 2 + 1);
     int max_depth = 0;
-    collapse(B, 0, 0, out, max_depth);
+    collapse(B, 0, 0, out, max_depth, empty_ref);
     return max_depth;
 }
 

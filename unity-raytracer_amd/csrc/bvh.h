@@ -39,7 +39,10 @@ struct BuildResult {
 
 // Collapse a BVH2 into 4-wide nodes (largest-area internal child expanded
 // first), leaves inlined into the child refs.  Returns the max depth.
-int collapse_bvh4(const BuildResult &B, std::vector<rtd::BvhNode4> &out);
+// empty_ref: the ref stored in unused slots (their boxes are +inf and are
+// only "entered" by NaN / zero-direction rays): a sentinel leaf, never a
+// node, so such rays cannot cycle.
+int collapse_bvh4(const BuildResult &B, std::vector<rtd::BvhNode4> &out, int empty_ref);
 
 // Build over prims (reordered in place).  Always produces >= 1 internal node
 // when prims is non-empty (a lone leaf hangs off the root beside an empty child).

@@ -1,0 +1,436 @@
+// lbvh.hip — on-device linear BVH build (see lbvh.h).
+#include "lbvh.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include "rt_math.h"
+
+namespace rtl {
+namespace {
+
+using rtm::f3;
+using rtm::mk;
+
+constexpr int kThreads = 256;
+
+inline int blocks_for(int n) { return (n + kThreads - 1) / kThreads; }
+
+__device__ __forceinline__ unsigned expand_bits(unsigned v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__device__ __forceinline__ unsigned morton30(f3 c, const LbvhInput &in) {
+    unsigned q[3];
+    const float lo[3] = {in.scene_lo[0], in.scene_lo[1], in.scene_lo[2]};
+    const float hi[3] = {in.scene_hi[0], in.scene_hi[1], in.scene_hi[2]};
+    const float cv[3] = {c.x, c.y, c.z};
+    for (int a = 0; a < 3; ++a) {
+        const float ext = hi[a] - lo[a];
+        float t = ext > 0.0f ? (cv[a] - lo[a]) / ext : 0.5f;
+        t = fminf(fmaxf(t, 0.0f), 1.0f);
+        q[a] = (unsigned)fminf(t * 1024.0f, 1023.0f);
+    }
+    return (expand_bits(q[0]) << 2) | (expand_bits(q[1]) << 1) | expand_bits(q[2]);
+}
+
+__device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+
+// 1. per reference rank: records, padded bounds, sort key
+__global__ void k_prims(LbvhInput in, LbvhOutput out, int n, float4 *plo, float4 *phi, unsigned long long *keys,
+                        int *vals, rtd::TriRec *tri_rank) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    float lo[3], hi[3], cen[3];
+    int gate = -1;
+    if (r < in.mt || r >= in.mt + in.ns) {
+        const float *v;
+        const float *nn;
+        int mat;
+        if (r < in.mt) {
+            int a = 0, b = in.mesh_count - 1;  // last mesh with rank_first <= r
+            while (a < b) {
+                const int m = (a + b + 1) >> 1;
+                if (in.meshes[m].rank_first <= r) a = m; else b = m - 1;
+            }
+            const MeshDev M = in.meshes[a];
+            const int g = M.geom_first + (r - M.rank_first);
+            v = in.mesh_tris + (size_t)g * 9;
+            nn = in.mesh_normals + (size_t)g * 3;
+            mat = M.material;
+            gate = a;
+        } else {
+            const int i = r - in.mt - in.ns;
+            v = in.loose_tris + (size_t)i * 9;
+            nn = in.loose_normals + (size_t)i * 3;
+            mat = in.loose_mat[i];
+        }
+        const f3 v0 = ld3(v), v1 = ld3(v + 3), v2 = ld3(v + 6);
+        const f3 e1 = v1 - v0, e2 = v2 - v0;  // RMath.cs:34-35
+        rtd::TriRec tr;
+        tr.p0 = make_float4(v0.x, v0.y, v0.z, e1.x);
+        tr.p1 = make_float4(e1.y, e1.z, e2.x, e2.y);
+        tr.p2 = make_float4(e2.z, __int_as_float(r), __int_as_float(gate), 0.0f);
+        tri_rank[r] = tr;
+        out.shade[r] = make_float4(nn[0], nn[1], nn[2], __int_as_float(mat));
+        float ext = 0.0f;
+        const float *vs[3] = {v, v + 3, v + 6};
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(vs[0][a], fminf(vs[1][a], vs[2][a]));
+            hi[a] = fmaxf(vs[0][a], fmaxf(vs[1][a], vs[2][a]));
+            ext = fmaxf(ext, hi[a] - lo[a]);
+        }
+        const float pad = in.pad_abs + ext * 1e-4f;
+        for (int a = 0; a < 3; ++a) {
+            cen[a] = 0.5f * (lo[a] + hi[a]);
+            lo[a] -= pad;
+            hi[a] += pad;
+        }
+    } else {
+        const int i = r - in.mt;
+        const float *sp = in.spheres + (size_t)i * 4;
+        const float rad = sqrtf(sp[3]);
+        rtd::SphRec sr;
+        sr.cr = make_float4(sp[0], sp[1], sp[2], sp[3]);
+        sr.misc = make_int4(r, -1, 0, 0);
+        *(rtd::SphRec *)&tri_rank[r] = sr;
+        out.shade[r] = make_float4(sp[0], sp[1], sp[2], __int_as_float(in.sphere_mat[i]));
+        const float pad = in.pad_abs + rad * 1e-4f;
+        for (int a = 0; a < 3; ++a) {
+            cen[a] = sp[a];
+            lo[a] = sp[a] - rad - pad;
+            hi[a] = sp[a] + rad + pad;
+        }
+    }
+    plo[r] = make_float4(lo[0], lo[1], lo[2], 0.0f);
+    phi[r] = make_float4(hi[0], hi[1], hi[2], 0.0f);
+    // Spatial order first; the mesh id only breaks ties so that a mesh's
+    // triangles in one Morton cell stay adjacent (mesh-major keys would put
+    // spatially scattered meshes side by side at the top of the tree).
+    keys[r] = ((unsigned long long)morton30(mk(cen[0], cen[1], cen[2]), in) << 32) | (unsigned)(gate + 1);
+    vals[r] = r;
+}
+
+__global__ void k_kind(LbvhInput in, int n, const int *sorted_rank, int *is_sph) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = sorted_rank[i];
+    is_sph[i] = (r >= in.mt && r < in.mt + in.ns) ? 1 : 0;
+}
+
+// 3. leaf-order primitive arrays, inline leaf refs, sorted boxes
+__global__ void k_leaves(LbvhInput in, LbvhOutput out, int n, const int *sorted_rank, const int *sph_idx,
+                         const rtd::TriRec *tri_rank, const float4 *plo, const float4 *phi, float4 *slo, float4 *shi,
+                         int *leaf_ref) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) out.tris[in.mt + in.nl] = rtd::sentinel_tri();
+    if (i >= n) return;
+    const int r = sorted_rank[i];
+    const bool sph = r >= in.mt && r < in.mt + in.ns;
+    const int si = sph_idx[i];
+    if (sph) {
+        out.sphs[si] = *(const rtd::SphRec *)&tri_rank[r];
+        leaf_ref[i] = rtd::encode_leaf(si, 1, rtd::kLeafSphere);
+    } else {
+        const int ti = i - si;
+        out.tris[ti] = tri_rank[r];
+        leaf_ref[i] = rtd::encode_leaf(ti, 1, rtd::kLeafTri);
+    }
+    slo[i] = plo[r];
+    shi[i] = phi[r];
+}
+
+__device__ __forceinline__ int delta(const unsigned long long *k, int n, int i, int j) {
+    if (j < 0 || j >= n) return -1;
+    const unsigned long long a = k[i], b = k[j];
+    if (a == b) return 64 + __clz(i ^ j);
+    return __clzll(a ^ b);
+}
+
+// 4. Karras 2012: internal node i covers a key range and splits it at the
+// highest differing bit; parents recorded as (node << 1 | side).
+__global__ void k_karras(int n, int empty_ref, const unsigned long long *k, const int *leaf_ref, const float4 *slo,
+                         const float4 *shi, rtd::BvhNode *nodes, int *leaf_parent, int *node_parent) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n == 1) {
+        if (i == 0) {  // lone leaf beside an empty slot (+inf box, sentinel leaf)
+            const float4 lo = slo[0], hi = shi[0];
+            const float inf = INFINITY;
+            rtd::BvhNode nd;
+            nd.a = make_float4(lo.x, hi.x, lo.y, hi.y);
+            nd.b = make_float4(inf, inf, inf, inf);
+            nd.c = make_float4(lo.z, hi.z, inf, inf);
+            nd.d = make_int4(leaf_ref[0], empty_ref, 0, 0);
+            nodes[0] = nd;
+        }
+        return;
+    }
+    if (i >= n - 1) return;
+    const int d = delta(k, n, i, i + 1) - delta(k, n, i, i - 1) >= 0 ? 1 : -1;
+    const int dmin = delta(k, n, i, i - d);
+    int lmax = 2;
+    while (delta(k, n, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta(k, n, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = delta(k, n, i, j);
+    int s = 0, t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (delta(k, n, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + (d < 0 ? -1 : 0);
+    const int first = min(i, j), last = max(i, j);
+    int left, right;
+    if (first == gamma) {
+        left = leaf_ref[gamma];
+        leaf_parent[gamma] = i << 1;
+    } else {
+        left = gamma;
+        node_parent[gamma] = i << 1;
+    }
+    if (last == gamma + 1) {
+        right = leaf_ref[gamma + 1];
+        leaf_parent[gamma + 1] = (i << 1) | 1;
+    } else {
+        right = gamma + 1;
+        node_parent[gamma + 1] = (i << 1) | 1;
+    }
+    nodes[i].d = make_int4(left, right, 0, 0);
+    if (i == 0) node_parent[0] = -1;
+}
+
+__device__ __forceinline__ void write_slot(rtd::BvhNode *nd, int side, float4 lo, float4 hi) {
+    float *a = side ? &nd->b.x : &nd->a.x;
+    a[0] = lo.x;
+    a[1] = hi.x;
+    a[2] = lo.y;
+    a[3] = hi.y;
+    float *c = &nd->c.x + 2 * side;
+    c[0] = lo.z;
+    c[1] = hi.z;
+}
+
+// 5. bottom-up boxes: each child writes its box into its parent's slot; the
+// second arrival (atomic counter) unions both slots and climbs.  Agent-scope
+// fences publish the slot before the count and make the sibling's slot
+// visible after it (per-XCD L2s and per-CU L1s are not coherent).
+__global__ void k_bounds(int n, const float4 *slo, const float4 *shi, const int *leaf_parent,
+                         const int *node_parent, rtd::BvhNode *nodes, int *flags) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n < 2 || i >= n) return;
+    float4 lo = slo[i], hi = shi[i];
+    int ps = leaf_parent[i];
+    while (ps >= 0) {
+        const int p = ps >> 1, side = ps & 1;
+        write_slot(&nodes[p], side, lo, hi);
+        __threadfence();
+        // release: the write-back must complete before the count is visible
+        // (MI355X_MICROARCH.md "Compiler hazard")
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(&flags[p], 1) == 0) return;
+        __threadfence();  // acquire: drop stale L1 copies of the sibling slot
+        const rtd::BvhNode nd = nodes[p];
+        float4 olo, ohi;
+        if (side) {  // sibling is slot 0
+            olo = make_float4(nd.a.x, nd.a.z, nd.c.x, 0.0f);
+            ohi = make_float4(nd.a.y, nd.a.w, nd.c.y, 0.0f);
+        } else {
+            olo = make_float4(nd.b.x, nd.b.z, nd.c.z, 0.0f);
+            ohi = make_float4(nd.b.y, nd.b.w, nd.c.w, 0.0f);
+        }
+        lo = make_float4(fminf(lo.x, olo.x), fminf(lo.y, olo.y), fminf(lo.z, olo.z), 0.0f);
+        hi = make_float4(fmaxf(hi.x, ohi.x), fmaxf(hi.y, ohi.y), fmaxf(hi.z, ohi.z), 0.0f);
+        ps = node_parent[p];
+    }
+}
+
+// 6. depth of every internal node (climb to the root; depths are small) and
+// the even-depth flag: even-depth nodes become 4-wide nodes.
+__global__ void k_depth(int n, const int *node_parent, int *even, int *max_depth) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    int d = 0;
+    for (int ps = node_parent[i]; ps >= 0; ps = node_parent[ps >> 1]) ++d;
+    even[i] = (d & 1) == 0;
+    // leaves sit one level below their parent
+    atomicMax(max_depth, d + 1);
+}
+
+__device__ __forceinline__ void read_slot(const rtd::BvhNode &nd, int side, float lo[3], float hi[3]) {
+    if (side) {
+        lo[0] = nd.b.x; hi[0] = nd.b.y; lo[1] = nd.b.z; hi[1] = nd.b.w; lo[2] = nd.c.z; hi[2] = nd.c.w;
+    } else {
+        lo[0] = nd.a.x; hi[0] = nd.a.y; lo[1] = nd.a.z; hi[1] = nd.a.w; lo[2] = nd.c.x; hi[2] = nd.c.y;
+    }
+}
+
+// 7. collapse: an even-depth node adopts its grandchildren through internal
+// children (leaf children keep their slot); unused slots get +inf boxes and
+// the sentinel leaf.  Child node refs are renumbered by the exclusive scan of
+// the even flags (the root stays 0).
+__global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, const int *even, const int *idx4,
+                           rtd::BvhNode4 *out, int *info) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) info[1] = n > 1 ? idx4[n - 2] + even[n - 2] : 1;  // 4-wide node count
+    if (i >= (n > 1 ? n - 1 : 1) || (n > 1 && !even[i])) return;
+    float lo[3][4], hi[3][4];
+    int ref[4];
+    int k = 0;
+    const rtd::BvhNode nd = nodes[i];
+    const int ch[2] = {nd.d.x, nd.d.y};
+    for (int s = 0; s < 2; ++s) {
+        if (ch[s] >= 0 && n > 1) {
+            const rtd::BvhNode cn = nodes[ch[s]];
+            const int gc[2] = {cn.d.x, cn.d.y};
+            for (int g = 0; g < 2; ++g) {
+                float l[3], h[3];
+                read_slot(cn, g, l, h);
+                for (int a = 0; a < 3; ++a) {
+                    lo[a][k] = l[a];
+                    hi[a][k] = h[a];
+                }
+                ref[k++] = gc[g] >= 0 ? idx4[gc[g]] : gc[g];
+            }
+        } else {
+            float l[3], h[3];
+            read_slot(nd, s, l, h);
+            for (int a = 0; a < 3; ++a) {
+                lo[a][k] = l[a];
+                hi[a][k] = h[a];
+            }
+            ref[k++] = ch[s];
+        }
+    }
+    for (; k < 4; ++k) {
+        for (int a = 0; a < 3; ++a) {
+            lo[a][k] = INFINITY;
+            hi[a][k] = INFINITY;
+        }
+        ref[k] = empty_ref;
+    }
+    rtd::BvhNode4 o;
+    o.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
+    o.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
+    o.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
+    o.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
+    o.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
+    o.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
+    o.child = make_int4(ref[0], ref[1], ref[2], ref[3]);
+    o.pad = make_int4(0, 0, 0, 0);
+    out[n > 1 ? idx4[i] : 0] = o;
+}
+
+struct Layout {
+    size_t keys_a, keys_b, vals_a, vals_b, plo, phi, tri_rank, is_sph, sph_idx, slo, shi, leaf_ref, leaf_parent,
+        node_parent, flags, even, idx4, depth, cub, total;
+    size_t cub_bytes;
+};
+
+size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+Layout layout(int n) {
+    Layout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off = align_up(off + bytes);
+        return o;
+    };
+    L.keys_a = take(sizeof(unsigned long long) * n);
+    L.keys_b = take(sizeof(unsigned long long) * n);
+    L.vals_a = take(sizeof(int) * n);
+    L.vals_b = take(sizeof(int) * n);
+    L.plo = take(sizeof(float4) * n);
+    L.phi = take(sizeof(float4) * n);
+    L.tri_rank = take(sizeof(rtd::TriRec) * n);
+    L.is_sph = take(sizeof(int) * n);
+    L.sph_idx = take(sizeof(int) * n);
+    L.slo = take(sizeof(float4) * n);
+    L.shi = take(sizeof(float4) * n);
+    L.leaf_ref = take(sizeof(int) * n);
+    L.leaf_parent = take(sizeof(int) * n);
+    L.node_parent = take(sizeof(int) * n);
+    L.flags = take(sizeof(int) * n);
+    L.even = take(sizeof(int) * n);
+    L.idx4 = take(sizeof(int) * n);
+    L.depth = take(2 * sizeof(int));  // depth, 4-wide node count
+    size_t sort_bytes = 0, scan_bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (unsigned long long *)nullptr,
+                                             (unsigned long long *)nullptr, (int *)nullptr, (int *)nullptr, n);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (int *)nullptr, (int *)nullptr, n);
+    L.cub_bytes = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
+    L.cub = take(L.cub_bytes);
+    L.total = off;
+    return L;
+}
+
+}  // namespace
+
+size_t lbvh_scratch_bytes(int n) { return layout(n < 1 ? 1 : n).total; }
+
+const int *lbvh_info_ptr(const void *scratch, int n) {
+    return (const int *)((const char *)scratch + layout(n < 1 ? 1 : n).depth);
+}
+
+hipError_t build_lbvh_gpu(const LbvhInput &in, const LbvhOutput &out, void *scratch, size_t scratch_bytes,
+                          hipStream_t stream) {
+    const int n = in.mt + in.ns + in.nl;
+    if (n < 1) return hipSuccess;
+    const Layout L = layout(n);
+    if (scratch_bytes < L.total) return hipErrorInvalidValue;
+    char *b = (char *)scratch;
+    auto *keys_a = (unsigned long long *)(b + L.keys_a), *keys_b = (unsigned long long *)(b + L.keys_b);
+    auto *vals_a = (int *)(b + L.vals_a), *vals_b = (int *)(b + L.vals_b);
+    auto *plo = (float4 *)(b + L.plo), *phi = (float4 *)(b + L.phi);
+    auto *tri_rank = (rtd::TriRec *)(b + L.tri_rank);
+    auto *is_sph = (int *)(b + L.is_sph), *sph_idx = (int *)(b + L.sph_idx);
+    auto *slo = (float4 *)(b + L.slo), *shi = (float4 *)(b + L.shi);
+    auto *leaf_ref = (int *)(b + L.leaf_ref), *leaf_parent = (int *)(b + L.leaf_parent);
+    auto *node_parent = (int *)(b + L.node_parent), *flags = (int *)(b + L.flags);
+    void *cub = b + L.cub;
+
+    hipLaunchKernelGGL(k_prims, dim3(blocks_for(n)), dim3(kThreads), 0, stream, in, out, n, plo, phi, keys_a, vals_a,
+                       tri_rank);
+    size_t cub_bytes = L.cub_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(cub, cub_bytes, keys_a, keys_b, vals_a, vals_b, n, 0,
+                                                      in.key_bits, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_kind, dim3(blocks_for(n)), dim3(kThreads), 0, stream, in, n, vals_b, is_sph);
+    cub_bytes = L.cub_bytes;
+    e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, is_sph, sph_idx, n, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_leaves, dim3(blocks_for(n)), dim3(kThreads), 0, stream, in, out, n, vals_b, sph_idx,
+                       tri_rank, plo, phi, slo, shi, leaf_ref);
+    hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n,
+                       rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), keys_b, leaf_ref, slo, shi,
+                       out.nodes, leaf_parent, node_parent);
+    e = hipMemsetAsync(flags, 0, sizeof(int) * n, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bounds, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, slo, shi, leaf_parent,
+                       node_parent, out.nodes, flags);
+    int *depth = (int *)(b + L.depth);
+    e = hipMemsetAsync(depth, 0, 2 * sizeof(int), stream);
+    if (e != hipSuccess) return e;
+    if (n > 1) {
+        int *even = (int *)(b + L.even), *idx4 = (int *)(b + L.idx4);
+        hipLaunchKernelGGL(k_depth, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, node_parent, even, depth);
+        if (out.nodes4) {
+            cub_bytes = L.cub_bytes;
+            e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, even, idx4, n - 1, stream);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(k_collapse, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n,
+                               rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, even, idx4, out.nodes4, depth);
+        }
+    } else if (out.nodes4) {
+        hipLaunchKernelGGL(k_collapse, dim3(1), dim3(kThreads), 0, stream, n,
+                           rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, nullptr, nullptr, out.nodes4, depth);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rtl

@@ -23,10 +23,31 @@
 
 #include "bvh.h"
 #include "kernels.h"
+#include "lbvh.h"
 #include "rt_device.h"
 #include "rt_math.h"
 
 namespace {
+
+struct GrowBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+// Device buffers of the GPU (LBVH) build path, kept across rebuilds.
+struct LbvhBufs {
+    GrowBuf meshes, mesh_tris, mesh_normals, spheres, sphere_mat, loose_tris, loose_normals, loose_mat;
+    GrowBuf nodes, nodes4, tris, sphs, shade, scratch;
+    void release() {
+        GrowBuf *all[] = {&meshes, &mesh_tris, &mesh_normals, &spheres, &sphere_mat, &loose_tris, &loose_normals,
+                          &loose_mat, &nodes, &nodes4, &tris, &sphs, &shade, &scratch};
+        for (GrowBuf *b : all) {
+            if (b->p) (void)hipFree(b->p);
+            b->p = nullptr;
+            b->cap = 0;
+        }
+    }
+};
 
 struct DeviceArrays {
     void *nodes = nullptr, *nodes4 = nullptr, *leaves = nullptr, *tris = nullptr, *sphs = nullptr, *shade = nullptr,
@@ -58,8 +79,9 @@ struct rt_ctx {
     int4 *wf_hit = nullptr;
     unsigned char *wf_occ = nullptr;
     size_t pool_cap = 0, shadow_cap = 0;
-    double last_build_ms = 0.0;
     int last_bvh_depth = 0;
+    rt_scene_info info{};
+    LbvhBufs lb;
 };
 
 namespace {
@@ -283,7 +305,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, float4
     F.out = d_out;
     F.counters = ctx->d_counters;
     const bool count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
-    const bool packet = (prm->flags & RT_FLAG_PACKET) != 0;
+    const bool packet = (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
     const bool wavefront = !packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
     const bool mega = !packet && !wavefront;  // default
     int chunk_tiles = 0;
@@ -324,6 +346,108 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, float4
         stats->total_ms =
             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
+    return RT_OK;
+}
+
+
+// Grow-only device buffer (per-frame rebuilds reuse their memory).
+hipError_t ensure(rt_ctx *ctx, GrowBuf &b, size_t bytes) {
+    (void)ctx;
+    if (bytes <= b.cap) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        if (e != hipSuccess) return e;
+    }
+    b.p = nullptr;
+    b.cap = 0;
+    hipError_t e = hipMalloc(&b.p, bytes < 256 ? 256 : bytes);
+    if (e == hipSuccess) b.cap = bytes < 256 ? 256 : bytes;
+    return e;
+}
+
+template <typename T>
+hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
+    hipError_t e = ensure(ctx, b, count * sizeof(T));
+    if (e != hipSuccess || count == 0) return e;
+    return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
+}
+
+// GPU LBVH path of rt_set_scene_ex: uploads the caller's arrays as they are
+// (no per-primitive host work beyond material ids) and builds on the device.
+template <typename MatId>
+int set_scene_lbvh(rt_ctx *ctx, const rt_scene_desc *sc, int MT, int NS, int NL, rtm::f3 smin, rtm::f3 smax,
+                   float pad_abs, MatId &mat_id, bool wide, rtd::SceneDev &S, int &nodes_count) {
+    const int P = MT + NS + NL;
+    std::vector<rtl::MeshDev> meshes((size_t)sc->mesh_count);
+    for (int m = 0; m < sc->mesh_count; ++m) {
+        meshes[m].rank_first = ctx->mesh_rank_first[m];
+        meshes[m].geom_first = sc->meshes[m].first_triangle;
+        meshes[m].count = sc->meshes[m].triangle_count;
+        meshes[m].material = mat_id(sc->meshes[m].material);
+    }
+    std::vector<int> sph_mat((size_t)NS), loose_mat((size_t)NL);
+    for (int i = 0; i < NS; ++i) sph_mat[i] = mat_id(sc->sphere_materials[i]);
+    for (int i = 0; i < NL; ++i) loose_mat[i] = mat_id(sc->triangle_materials[i]);
+    LbvhBufs &B = ctx->lb;
+    HIP_OR_FAIL(ctx, put(ctx, B.meshes, meshes.data(), meshes.size()));
+    HIP_OR_FAIL(ctx, put(ctx, B.mesh_tris, sc->mesh_triangles, (size_t)sc->mesh_triangle_total));
+    HIP_OR_FAIL(ctx, put(ctx, B.mesh_normals, sc->mesh_triangle_normals, (size_t)sc->mesh_triangle_total));
+    HIP_OR_FAIL(ctx, put(ctx, B.spheres, sc->spheres, (size_t)NS));
+    HIP_OR_FAIL(ctx, put(ctx, B.sphere_mat, sph_mat.data(), sph_mat.size()));
+    HIP_OR_FAIL(ctx, put(ctx, B.loose_tris, sc->triangles, (size_t)NL));
+    HIP_OR_FAIL(ctx, put(ctx, B.loose_normals, sc->triangle_normals, (size_t)NL));
+    HIP_OR_FAIL(ctx, put(ctx, B.loose_mat, loose_mat.data(), loose_mat.size()));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.nodes, sizeof(rtd::BvhNode) * (size_t)std::max(1, P - 1)));
+    if (wide) HIP_OR_FAIL(ctx, ensure(ctx, B.nodes4, sizeof(rtd::BvhNode4) * (size_t)std::max(1, P - 1)));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.tris, sizeof(rtd::TriRec) * (size_t)(MT + NL + 1)));  // + sentinel
+    HIP_OR_FAIL(ctx, ensure(ctx, B.sphs, sizeof(rtd::SphRec) * (size_t)std::max(1, NS)));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.shade, sizeof(float4) * (size_t)P));
+    const size_t scratch = rtl::lbvh_scratch_bytes(P);
+    HIP_OR_FAIL(ctx, ensure(ctx, B.scratch, scratch));
+    rtl::LbvhInput in{};
+    in.mesh_count = sc->mesh_count;
+    in.mt = MT;
+    in.ns = NS;
+    in.nl = NL;
+    in.meshes = (const rtl::MeshDev *)B.meshes.p;
+    in.mesh_tris = (const float *)B.mesh_tris.p;
+    in.mesh_normals = (const float *)B.mesh_normals.p;
+    in.spheres = (const float *)B.spheres.p;
+    in.sphere_mat = (const int *)B.sphere_mat.p;
+    in.loose_tris = (const float *)B.loose_tris.p;
+    in.loose_normals = (const float *)B.loose_normals.p;
+    in.loose_mat = (const int *)B.loose_mat.p;
+    in.scene_lo[0] = smin.x; in.scene_lo[1] = smin.y; in.scene_lo[2] = smin.z;
+    in.scene_hi[0] = smax.x; in.scene_hi[1] = smax.y; in.scene_hi[2] = smax.z;
+    in.pad_abs = pad_abs;
+    in.key_bits = 62;
+    rtl::LbvhOutput out{};
+    out.nodes = (rtd::BvhNode *)B.nodes.p;
+    out.nodes4 = wide ? (rtd::BvhNode4 *)B.nodes4.p : nullptr;
+    out.tris = (rtd::TriRec *)B.tris.p;
+    out.sphs = (rtd::SphRec *)B.sphs.p;
+    out.shade = (float4 *)B.shade.p;
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_OR_FAIL(ctx, rtl::build_lbvh_gpu(in, out, B.scratch.p, B.scratch.cap, ctx->stream));
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0.0f;
+    HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->info.build_ms = ms;
+    int binfo[2] = {0, 0};
+    HIP_OR_FAIL(ctx, hipMemcpy(binfo, rtl::lbvh_info_ptr(B.scratch.p, P), sizeof(binfo), hipMemcpyDeviceToHost));
+    ctx->last_bvh_depth = binfo[0];
+    // traversal stack: one entry per 2-wide level, three per 4-wide level
+    const int need = wide ? 3 * ((binfo[0] + 1) / 2 + 1) : binfo[0] + 1;
+    if (need > rtd::kStackTotal)
+        return fail(ctx, RT_E_SCENE, "LBVH depth %d exceeds the traversal stack; use RT_BUILD_SAH_HOST", binfo[0]);
+    S.nodes = (const rtd::BvhNode *)B.nodes.p;
+    S.nodes4 = wide ? (const rtd::BvhNode4 *)B.nodes4.p : nullptr;
+    S.tris = (const rtd::TriRec *)B.tris.p;
+    S.sphs = (const rtd::SphRec *)B.sphs.p;
+    S.shade = (const float4 *)B.shade.p;
+    S.bvh4 = wide ? 1 : 0;
+    nodes_count = wide ? binfo[1] : std::max(1, P - 1);
     return RT_OK;
 }
 
@@ -372,6 +496,7 @@ void rt_destroy(rt_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     free_scene(ctx);
     free_wavefront(ctx);
+    ctx->lb.release();
     if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
@@ -394,9 +519,14 @@ int rt_set_stream(rt_ctx *ctx, void *hip_stream) {
     return RT_OK;
 }
 
-int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
+int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) { return rt_set_scene_ex(ctx, sc, RT_BUILD_SAH_HOST); }
+
+int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
     if (!ctx) return RT_E_INVALID;
+    auto t_start = std::chrono::steady_clock::now();
     if (!sc) return fail(ctx, RT_E_INVALID, "scene is null");
+    if (build != RT_BUILD_SAH_HOST && build != RT_BUILD_LBVH_GPU && build != RT_BUILD_LBVH_GPU_BVH2)
+        return fail(ctx, RT_E_INVALID, "unknown build %d", build);
     if (sc->triangle_count < 0 || sc->mesh_triangle_total < 0 || sc->mesh_count < 0 || sc->sphere_count < 0 ||
         sc->point_light_count < 0)
         return fail(ctx, RT_E_INVALID, "negative count in scene");
@@ -415,11 +545,12 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
                         M.first_triangle, M.triangle_count, sc->mesh_triangle_total);
         mesh_ranks += M.triangle_count;
     }
-    if (mesh_ranks + sc->sphere_count + sc->triangle_count > (int64_t)(1 << 30))
-        return fail(ctx, RT_E_SCENE, "too many primitives");
+    if (mesh_ranks + sc->sphere_count + sc->triangle_count > (int64_t)(1 << rtd::kLeafFirstBits))
+        return fail(ctx, RT_E_SCENE, "too many primitives (max %d)", 1 << rtd::kLeafFirstBits);
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     free_scene(ctx);
+    ctx->info = rt_scene_info{};
 
     const int MT = (int)mesh_ranks, NS = sc->sphere_count, NL = sc->triangle_count;
     const int P = MT + NS + NL;
@@ -457,113 +588,20 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
         mats.push_back(to_dev(m));
         return id;
     };
-
-    // Per-rank source geometry + shading record; primitives for the builder.
-    struct TriSrc { rtm::f3 v0, v1, v2; };
-    std::vector<TriSrc> tri_src((size_t)P);
-    std::vector<float4> shade((size_t)P);
-    std::vector<rtb::Prim> prims;
-    prims.reserve((size_t)P);
     float scale = 1.0f;
     for (float v : {smin.x, smin.y, smin.z, smax.x, smax.y, smax.z})
         if (std::isfinite(v)) scale = std::max(scale, std::fabs(v));
     const float pad_abs = scale * 0x1p-13f;
-    auto add_tri_prim = [&](int rank, const rt_triangle &t, int gate) {
-        rtb::Prim p;
-        const float *v[3] = {&t.vertex0.x, &t.vertex1.x, &t.vertex2.x};
-        float ext = 0.0f;
-        for (int a = 0; a < 3; ++a) {
-            p.lo[a] = std::min(v[0][a], std::min(v[1][a], v[2][a]));
-            p.hi[a] = std::max(v[0][a], std::max(v[1][a], v[2][a]));
-            ext = std::max(ext, p.hi[a] - p.lo[a]);
-        }
-        const float pad = pad_abs + ext * 1e-4f;
-        for (int a = 0; a < 3; ++a) {
-            p.c[a] = 0.5f * (p.lo[a] + p.hi[a]);
-            p.lo[a] -= pad;
-            p.hi[a] += pad;
-        }
-        p.kind = rtd::kLeafTri;
-        p.gate = gate;
-        p.payload = rank;
-        tri_src[rank] = {F3(t.vertex0), F3(t.vertex1), F3(t.vertex2)};
-        prims.push_back(p);
-    };
+
     ctx->mesh_rank_first.assign((size_t)sc->mesh_count + 1, 0);
-    int rank = 0;
-    for (int m = 0; m < sc->mesh_count; ++m) {
-        const rt_mesh &M = sc->meshes[m];
-        ctx->mesh_rank_first[m] = rank;
-        const int mid = mat_id(M.material);
-        for (int i = 0; i < M.triangle_count; ++i, ++rank) {
-            const int g = M.first_triangle + i;
-            add_tri_prim(rank, sc->mesh_triangles[g], m);
-            const rt_float3 &nn = sc->mesh_triangle_normals[g];
-            int bits;
-            std::memcpy(&bits, &mid, 4);
-            shade[rank] = make_float4(nn.x, nn.y, nn.z, 0.0f);
-            std::memcpy(&shade[rank].w, &bits, 4);
+    {
+        int rk = 0;
+        for (int m = 0; m < sc->mesh_count; ++m) {
+            ctx->mesh_rank_first[m] = rk;
+            rk += sc->meshes[m].triangle_count;
         }
+        ctx->mesh_rank_first[sc->mesh_count] = rk;
     }
-    ctx->mesh_rank_first[sc->mesh_count] = rank;
-    std::vector<rtd::SphRec> sph_src((size_t)NS);
-    for (int i = 0; i < NS; ++i, ++rank) {
-        const rt_sphere &s = sc->spheres[i];
-        const float r = sqrtf(s.radius_squared);
-        rtb::Prim p;
-        const float c[3] = {s.center.x, s.center.y, s.center.z};
-        const float pad = pad_abs + r * 1e-4f;
-        for (int a = 0; a < 3; ++a) {
-            p.c[a] = c[a];
-            p.lo[a] = c[a] - r - pad;
-            p.hi[a] = c[a] + r + pad;
-        }
-        p.kind = rtd::kLeafSphere;
-        p.gate = -1;
-        p.payload = rank;
-        prims.push_back(p);
-        sph_src[i].cr = make_float4(s.center.x, s.center.y, s.center.z, s.radius_squared);
-        sph_src[i].misc = make_int4(rank, -1, 0, 0);
-        const int mid = mat_id(sc->sphere_materials[i]);
-        shade[rank] = make_float4(s.center.x, s.center.y, s.center.z, 0.0f);
-        std::memcpy(&shade[rank].w, &mid, 4);
-    }
-    for (int i = 0; i < NL; ++i, ++rank) {
-        add_tri_prim(rank, sc->triangles[i], -1);
-        const rt_float3 &nn = sc->triangle_normals[i];
-        const int mid = mat_id(sc->triangle_materials[i]);
-        shade[rank] = make_float4(nn.x, nn.y, nn.z, 0.0f);
-        std::memcpy(&shade[rank].w, &mid, 4);
-    }
-
-    rtb::BuildResult B = rtb::build_bvh(prims, 4);
-    ctx->last_build_ms = B.build_ms;
-    ctx->last_bvh_depth = B.max_depth;
-    if (B.max_depth > rtd::kMaxTreeDepth)
-        return fail(ctx, RT_E_INTERNAL, "BVH depth %d exceeds stack", B.max_depth);
-    std::vector<rtd::BvhNode4> nodes4;
-    const int depth4 = rtb::collapse_bvh4(B, nodes4);
-    if (3 * (depth4 + 1) > rtd::kStackTotal)
-        return fail(ctx, RT_E_INTERNAL, "BVH4 depth %d exceeds stack", depth4);
-    std::vector<int> tri_gate((size_t)P, -1);
-    for (int m = 0; m < sc->mesh_count; ++m)
-        for (int r = ctx->mesh_rank_first[m]; r < ctx->mesh_rank_first[m + 1]; ++r) tri_gate[r] = m;
-
-    std::vector<rtd::TriRec> tris(B.tri_order.size());
-    for (size_t i = 0; i < B.tri_order.size(); ++i) {
-        const int rk = B.tri_order[i];
-        const TriSrc &t = tri_src[rk];
-        const rtm::f3 e1 = t.v1 - t.v0, e2 = t.v2 - t.v0;  // RMath.cs:34-35
-        float rbits;
-        std::memcpy(&rbits, &rk, 4);
-        tris[i].p0 = make_float4(t.v0.x, t.v0.y, t.v0.z, e1.x);
-        tris[i].p1 = make_float4(e1.y, e1.z, e2.x, e2.y);
-        float gbits;
-        std::memcpy(&gbits, &tri_gate[rk], 4);
-        tris[i].p2 = make_float4(e2.z, rbits, gbits, 0.0f);
-    }
-    std::vector<rtd::SphRec> sphs(B.sph_order.size());
-    for (size_t i = 0; i < B.sph_order.size(); ++i) sphs[i] = sph_src[B.sph_order[i] - MT];
     std::vector<rtd::MeshGate> gates((size_t)sc->mesh_count);
     for (int m = 0; m < sc->mesh_count; ++m) {
         const rt_aabb &a = sc->meshes[m].aabb;
@@ -577,30 +615,133 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
         lights[l].intensity = make_float4(L.intensity.x, L.intensity.y, L.intensity.z, 0.0f);
     }
 
-    HIP_OR_FAIL(ctx, upload(&ctx->arr.nodes, B.nodes));
-    HIP_OR_FAIL(ctx, upload(&ctx->arr.nodes4, nodes4));
-    HIP_OR_FAIL(ctx, upload(&ctx->arr.leaves, B.leaves));
-    HIP_OR_FAIL(ctx, upload(&ctx->arr.tris, tris));
-    HIP_OR_FAIL(ctx, upload(&ctx->arr.sphs, sphs));
-    HIP_OR_FAIL(ctx, upload(&ctx->arr.shade, shade));
+    rtd::SceneDev &S = ctx->S;
+    int nodes_count = 0;
+    if ((build == RT_BUILD_LBVH_GPU || build == RT_BUILD_LBVH_GPU_BVH2) && P > 0) {
+        const int st = set_scene_lbvh(ctx, sc, MT, NS, NL, smin, smax, pad_abs, mat_id,
+                                      build == RT_BUILD_LBVH_GPU, S, nodes_count);
+        if (st) return st;
+    } else {
+        // Host binned-SAH build (bvh.cpp), collapsed to 4-wide nodes.
+        struct TriSrc { rtm::f3 v0, v1, v2; };
+        std::vector<TriSrc> tri_src((size_t)P);
+        std::vector<float4> shade((size_t)P);
+        std::vector<rtb::Prim> prims;
+        prims.reserve((size_t)P);
+        auto add_tri_prim = [&](int rank, const rt_triangle &t, int gate) {
+            rtb::Prim p;
+            const float *v[3] = {&t.vertex0.x, &t.vertex1.x, &t.vertex2.x};
+            float ext = 0.0f;
+            for (int a = 0; a < 3; ++a) {
+                p.lo[a] = std::min(v[0][a], std::min(v[1][a], v[2][a]));
+                p.hi[a] = std::max(v[0][a], std::max(v[1][a], v[2][a]));
+                ext = std::max(ext, p.hi[a] - p.lo[a]);
+            }
+            const float pad = pad_abs + ext * 1e-4f;
+            for (int a = 0; a < 3; ++a) {
+                p.c[a] = 0.5f * (p.lo[a] + p.hi[a]);
+                p.lo[a] -= pad;
+                p.hi[a] += pad;
+            }
+            p.kind = rtd::kLeafTri;
+            p.gate = gate;
+            p.payload = rank;
+            tri_src[rank] = {F3(t.vertex0), F3(t.vertex1), F3(t.vertex2)};
+            prims.push_back(p);
+        };
+        auto put_shade = [&](int rank, float x, float y, float z, int mid) {
+            shade[rank] = make_float4(x, y, z, 0.0f);
+            std::memcpy(&shade[rank].w, &mid, 4);
+        };
+        int rank = 0;
+        for (int m = 0; m < sc->mesh_count; ++m) {
+            const rt_mesh &M = sc->meshes[m];
+            const int mid = mat_id(M.material);
+            for (int i = 0; i < M.triangle_count; ++i, ++rank) {
+                const int g = M.first_triangle + i;
+                add_tri_prim(rank, sc->mesh_triangles[g], m);
+                const rt_float3 &nn = sc->mesh_triangle_normals[g];
+                put_shade(rank, nn.x, nn.y, nn.z, mid);
+            }
+        }
+        std::vector<rtd::SphRec> sph_src((size_t)NS);
+        for (int i = 0; i < NS; ++i, ++rank) {
+            const rt_sphere &s = sc->spheres[i];
+            const float r = sqrtf(s.radius_squared);
+            rtb::Prim p;
+            const float c[3] = {s.center.x, s.center.y, s.center.z};
+            const float pad = pad_abs + r * 1e-4f;
+            for (int a = 0; a < 3; ++a) {
+                p.c[a] = c[a];
+                p.lo[a] = c[a] - r - pad;
+                p.hi[a] = c[a] + r + pad;
+            }
+            p.kind = rtd::kLeafSphere;
+            p.gate = -1;
+            p.payload = rank;
+            prims.push_back(p);
+            sph_src[i].cr = make_float4(s.center.x, s.center.y, s.center.z, s.radius_squared);
+            sph_src[i].misc = make_int4(rank, -1, 0, 0);
+            put_shade(rank, s.center.x, s.center.y, s.center.z, mat_id(sc->sphere_materials[i]));
+        }
+        for (int i = 0; i < NL; ++i, ++rank) {
+            add_tri_prim(rank, sc->triangles[i], -1);
+            const rt_float3 &nn = sc->triangle_normals[i];
+            put_shade(rank, nn.x, nn.y, nn.z, mat_id(sc->triangle_materials[i]));
+        }
+
+        rtb::BuildResult B = rtb::build_bvh(prims, 4);
+        ctx->last_bvh_depth = B.max_depth;
+        if (B.max_depth > rtd::kMaxTreeDepth)
+            return fail(ctx, RT_E_INTERNAL, "BVH depth %d exceeds stack", B.max_depth);
+        std::vector<rtd::BvhNode4> nodes4;
+        const int sentinel = (int)B.tri_order.size();
+        const int depth4 = rtb::collapse_bvh4(B, nodes4, rtd::encode_leaf(sentinel, 1, rtd::kLeafTri));
+        if (3 * (depth4 + 1) > rtd::kStackTotal)
+            return fail(ctx, RT_E_INTERNAL, "BVH4 depth %d exceeds stack", depth4);
+        std::vector<int> tri_gate((size_t)P, -1);
+        for (int m = 0; m < sc->mesh_count; ++m)
+            for (int r = ctx->mesh_rank_first[m]; r < ctx->mesh_rank_first[m + 1]; ++r) tri_gate[r] = m;
+        std::vector<rtd::TriRec> tris(B.tri_order.size());
+        for (size_t i = 0; i < B.tri_order.size(); ++i) {
+            const int rk = B.tri_order[i];
+            const TriSrc &t = tri_src[rk];
+            const rtm::f3 e1 = t.v1 - t.v0, e2 = t.v2 - t.v0;  // RMath.cs:34-35
+            float rbits, gbits;
+            std::memcpy(&rbits, &rk, 4);
+            std::memcpy(&gbits, &tri_gate[rk], 4);
+            tris[i].p0 = make_float4(t.v0.x, t.v0.y, t.v0.z, e1.x);
+            tris[i].p1 = make_float4(e1.y, e1.z, e2.x, e2.y);
+            tris[i].p2 = make_float4(e2.z, rbits, gbits, 0.0f);
+        }
+        tris.push_back(rtd::sentinel_tri());
+        std::vector<rtd::SphRec> sphs(B.sph_order.size());
+        for (size_t i = 0; i < B.sph_order.size(); ++i) sphs[i] = sph_src[B.sph_order[i] - MT];
+        HIP_OR_FAIL(ctx, upload(&ctx->arr.nodes4, nodes4));
+        HIP_OR_FAIL(ctx, upload(&ctx->arr.tris, tris));
+        HIP_OR_FAIL(ctx, upload(&ctx->arr.sphs, sphs));
+        HIP_OR_FAIL(ctx, upload(&ctx->arr.shade, shade));
+        S.nodes = nullptr;
+        S.nodes4 = (const rtd::BvhNode4 *)ctx->arr.nodes4;
+        S.tris = (const rtd::TriRec *)ctx->arr.tris;
+        S.sphs = (const rtd::SphRec *)ctx->arr.sphs;
+        S.shade = (const float4 *)ctx->arr.shade;
+        S.bvh4 = 1;
+        nodes_count = (int)nodes4.size();
+    }
     HIP_OR_FAIL(ctx, upload(&ctx->arr.mats, mats));
     HIP_OR_FAIL(ctx, upload(&ctx->arr.lights, lights));
     HIP_OR_FAIL(ctx, upload(&ctx->arr.gates, gates));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
 
-    rtd::SceneDev &S = ctx->S;
-    S.nodes = (const rtd::BvhNode *)ctx->arr.nodes;
-    S.nodes4 = (const rtd::BvhNode4 *)ctx->arr.nodes4;
-    S.leaves = (const rtd::LeafDesc *)ctx->arr.leaves;
-    S.tris = (const rtd::TriRec *)ctx->arr.tris;
-    S.sphs = (const rtd::SphRec *)ctx->arr.sphs;
-    S.shade = (const float4 *)ctx->arr.shade;
+    S.leaves = nullptr;
     S.mats = (const rtd::DevMaterial *)ctx->arr.mats;
     S.lights = (const rtd::DevLight *)ctx->arr.lights;
     S.gates = (const rtd::MeshGate *)ctx->arr.gates;
     S.num_lights = sc->point_light_count;
     S.mesh_tri_total = MT;
     S.sphere_count = NS;
-    S.has_prims = P > 0 && !B.nodes.empty();
+    S.has_prims = P > 0;
     S.scene_lo[0] = smin.x; S.scene_lo[1] = smin.y; S.scene_lo[2] = smin.z;
     S.scene_hi[0] = smax.x; S.scene_hi[1] = smax.y; S.scene_hi[2] = smax.z;
     S.ambient[0] = sc->ambient_radiance.x;
@@ -610,7 +751,20 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
     ctx->mesh_tri_ranks = MT;
     ctx->sphere_count = NS;
     ctx->loose_count = NL;
+    ctx->info.build = build;
+    ctx->info.bvh_width = P > 0 ? (S.bvh4 ? 4 : 2) : 0;
+    ctx->info.nodes = P > 0 ? nodes_count : 0;
+    ctx->info.primitives = P;
+    ctx->info.total_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     ctx->has_scene = true;
+    return RT_OK;
+}
+
+int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info) {
+    if (!ctx || !info) return RT_E_INVALID;
+    if (!ctx->has_scene) return RT_E_STATE;
+    *info = ctx->info;
     return RT_OK;
 }
 

@@ -28,11 +28,8 @@ namespace rtd {
 #ifndef RT_STACK_LDS
 #define RT_STACK_LDS 24
 #endif
-#ifndef RT_BVH4
-#define RT_BVH4 1
-#endif
 constexpr int kStackSize = RT_STACK_LDS;  // LDS traversal stack entries per lane
-constexpr int kStackTotal = 96;           // + private (scratch) overflow; >= 3 * max BVH4 depth
+constexpr int kStackTotal = 128;          // + private (scratch) overflow: >= 3 * BVH4 depth, >= LBVH depth
 constexpr int kMaxTreeDepth = 31;         // builder guarantees BVH2 internal depth <= 31
 constexpr int kMaxBounces = 32;     // per-lane mirror fold stack
 constexpr int kWaveSize = 64;
@@ -52,7 +49,7 @@ struct alignas(16) BvhNode {
     float4 a;  // child0 lo.x, hi.x, lo.y, hi.y
     float4 b;  // child1 lo.x, hi.x, lo.y, hi.y
     float4 c;  // child0 lo.z, hi.z, child1 lo.z, hi.z
-    int4 d;    // child0, child1 (>= 0 internal node, < 0 leaf ~index), unused
+    int4 d;    // child0, child1 (>= 0 internal node, < 0 inline leaf ref), unused
 };
 
 // 4-wide node (BVH2 collapsed, 128 B = one L2 line): the four child boxes
@@ -82,6 +79,23 @@ struct alignas(16) TriRec {
     float4 p1;  // e1.y e1.z e2.x e2.y
     float4 p2;  // e2.z rank(bits) gate(bits: mesh index or -1) -
 };
+
+// Every scene's triangle array ends with a sentinel record: all-zero edges
+// and gate -1, so Moller-Trumbore rejects it for every ray (det == 0, or NaN
+// for a NaN ray).  Unused BVH child slots (+inf boxes) point at it: a NaN or
+// zero-direction ray that "enters" such a slot reaches a harmless leaf
+// instead of cycling back to the root.
+__host__ __device__ __forceinline__ TriRec sentinel_tri() {
+    TriRec t;
+    t.p0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    t.p1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int rank = 0x7fffffff, gate = -1;
+    float rb, gb;
+    __builtin_memcpy(&rb, &rank, 4);
+    __builtin_memcpy(&gb, &gate, 4);
+    t.p2 = make_float4(0.0f, rb, gb, 0.0f);
+    return t;
+}
 
 struct alignas(16) SphRec {
     float4 cr;  // center.xyz, radius_squared
@@ -120,6 +134,7 @@ struct SceneDev {
     int mesh_tri_total;  // ranks [0, mesh_tri_total) are mesh triangles
     int sphere_count;    // ranks [mesh_tri_total, +sphere_count) are spheres
     int has_prims;       // 0 → every ray misses after the scene gate
+    int bvh4;            // 1: nodes4 (host SAH build), 0: nodes (BVH2, GPU LBVH build)
     float scene_lo[3];   // Scene.AABB (Scene.CalculateAABB)
     float scene_hi[3];
     float ambient[3];    // AmbientLight.Radiance

@@ -246,8 +246,7 @@ __device__ __forceinline__ float child_key(float lx, float hx, float ly, float h
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
                                           const Stack &st, Counts &cnt) {
-    if (t.node >= 0) {
-#if RT_BVH4
+    if (t.node >= 0 && S.bvh4) {
         const rtd::BvhNode4 *np = S.nodes4 + t.node;
         const float4 lx = np->lox, hx = np->hix, ly = np->loy, hy = np->hiy, lz = np->loz, hz = np->hiz;
         const int4 ch = np->child;
@@ -299,7 +298,7 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
             t.node = c0;
             return false;
         }
-#else
+    } else if (t.node >= 0) {
         const rtd::BvhNode *np = S.nodes + t.node;
         const float4 a = np->a, b = np->b, c = np->c;
         const int4 ch = np->d;
@@ -317,18 +316,12 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
             t.node = h0 ? ch.x : ch.y;
             return false;
         }
-#endif
     } else {
-#if RT_BVH4
         const int v = ~t.node;
         const int first = v & ((1 << rtd::kLeafFirstBits) - 1);
         const int count = ((v >> rtd::kLeafFirstBits) & 3) + 1;
         const int kind = (v >> (rtd::kLeafFirstBits + 2)) & 1;
         const int gate = kind == rtd::kLeafTri ? __float_as_int(S.tris[first].p2.z) : S.sphs[first].misc.y;
-#else
-        const rtd::LeafDesc L = S.leaves[~t.node];
-        const int first = L.first, count = L.count, kind = L.kind, gate = L.gate;
-#endif
         if (leaf<ANY, COUNT>(S, r, t, d2, first, count, kind, gate, cnt)) return true;
     }
     return !pop(t, st);

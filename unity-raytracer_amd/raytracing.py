@@ -78,10 +78,17 @@ class Context:
     def set_stream(self, stream_handle: int):
         self._check(self.lib.rt_set_stream(self.h, C.c_void_p(stream_handle)))
 
-    def set_scene(self, scene: Scene):
+    def set_scene(self, scene: Scene, build: int = abi.RT_BUILD_SAH_HOST):
+        """Upload a scene and build its BVH: host SAH (4-wide) or on-device
+        LBVH (2-wide, for per-frame rebuilds).  Renders are identical."""
         desc = scene.to_desc()
-        self._check(self.lib.rt_set_scene(self.h, desc.ref()))
+        self._check(self.lib.rt_set_scene_ex(self.h, desc.ref(), int(build)))
         self._scene_desc = desc  # keep arrays alive for the duration of the call only; harmless
+
+    def scene_info(self) -> dict:
+        info = abi.rt_scene_info()
+        self._check(self.lib.rt_get_scene_info(self.h, C.byref(info)))
+        return info.as_dict()
 
     def render(self, camera: CameraData, plane: ImagePlane, params: abi.rt_render_params,
                out: Optional[np.ndarray] = None):
@@ -134,7 +141,7 @@ class RayTracingSetup:
 
     def __init__(self, scene: Scene, image_plane: ImagePlane, background_color=(0, 0, 0, 1),
                  max_reflection_bounces: int = 0, samples_per_pixel: int = 1,
-                 context: Optional[Context] = None):
+                 context: Optional[Context] = None, build: int = abi.RT_BUILD_SAH_HOST):
         self.Scene = scene
         self.ImagePlane = image_plane
         self.BackgroundColor = tuple(background_color)
@@ -143,6 +150,7 @@ class RayTracingSetup:
         self.PixelColors = np.zeros((0, 4), np.float32)
         self.ctx = context or Context()
         self.LastStats: Optional[abi.rt_stats] = None
+        self.Build = int(build)
         self.UpdateScene()
 
     @classmethod
@@ -152,7 +160,7 @@ class RayTracingSetup:
     def UpdateScene(self):
         """Upload Scene (replaces UpdateScene()'s result, :120-128; the
         library computes Scene.CalculateAABB and the BVH)."""
-        self.ctx.set_scene(self.Scene)
+        self.ctx.set_scene(self.Scene, self.Build)
 
     def CastPixelRays(self, camera: CameraData, flags: int = 0) -> np.ndarray:
         """:275-302 — fills PixelColors (resX*resY RGBA, index x + y*resX)."""
