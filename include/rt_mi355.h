@@ -221,6 +221,34 @@ typedef struct rt_scene_info {
 
 int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info);
 
+/* One mesh as the reference holds it before extraction: SceneMesh's
+ * MeshFilter.sharedMesh (vertices, index buffer) and Transform
+ * (SceneMesh.cs:11-53).  The device applies localToWorldMatrix with
+ * MultiplyPoint3x4, takes Mesh.AABB over all transformed vertices, builds the
+ * triangles in index-buffer order and their normals (-Triangle.Normal). */
+typedef struct rt_mesh_source {
+    const rt_float3 *vertices;  /* local space, vertex_count */
+    int32_t vertex_count;
+    const int32_t *indices;     /* triangle list, index_count = 3 x triangles, each in [0, vertex_count) */
+    int32_t index_count;
+    float local_to_world[16];   /* Transform.localToWorldMatrix, row-major: m[row * 4 + col] */
+    rt_material material;       /* SceneMesh.MaterialData */
+} rt_mesh_source;
+
+/* Scene whose meshes are extracted on the device (the replacement of
+ * UpdateScene's per-frame FetchMeshes, RayTracingSetup.cs:120-128,159-169).
+ * `base` carries the loose triangles, spheres, point lights and ambient light;
+ * its mesh fields must be empty.  Vertices and index buffers stay resident on
+ * the device; the BVH is built on the device (RT_BUILD_LBVH_GPU).  Results
+ * equal rt_set_scene with the same meshes extracted on the host. */
+int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count);
+
+/* Per-frame update of a scene set by rt_set_scene_source: new
+ * localToWorld matrices (mesh_count x 16 floats, rt_mesh_source layout),
+ * re-extraction and BVH rebuild on the device.  Only the matrices cross
+ * PCIe. */
+int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count);
+
 /* Render one frame: the MI355X replacement of CastPixelRays (:275-302).
  * out_rgba is a caller-owned HOST buffer of resolution_x*resolution_y*4
  * floats (row-major, y = 0 is the top row, alpha = 1), i.e. PixelColors.

@@ -23,7 +23,7 @@ def test_header_declares_expected_entry_points():
     names = _declared_functions()
     for n in ("rt_create", "rt_destroy", "rt_set_scene", "rt_render", "rt_render_device",
               "rt_last_error", "rt_intersect_rays", "rt_assemble_bands", "rt_abi_version",
-              "rt_set_scene_ex", "rt_get_scene_info"):
+              "rt_set_scene_ex", "rt_get_scene_info", "rt_set_scene_source", "rt_update_mesh_transforms"):
         assert n in names
 
 
@@ -44,7 +44,7 @@ def test_ctypes_layouts(rt):
     a = rt.abi
     sizes = {
         a.rt_float3: 12, a.rt_triangle: 36, a.rt_sphere: 16, a.rt_aabb: 24, a.rt_material: 56,
-        a.rt_point_light: 24, a.rt_camera: 48, a.rt_scene_info: 32, a.rt_image_plane: 20, a.rt_mesh: 88, a.rt_hit: 16,
+        a.rt_point_light: 24, a.rt_camera: 48, a.rt_scene_info: 32, a.rt_mesh_source: 152, a.rt_image_plane: 20, a.rt_mesh: 88, a.rt_hit: 16,
         a.rt_ray: 24, a.rt_render_params: 40, a.rt_stats: 72,
     }
     for t, s in sizes.items():
@@ -59,9 +59,10 @@ def test_c_layouts_match(tmp_path):
 #include <stddef.h>
 #include "rt_mi355.h"
 int main(void){
- printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_mesh), sizeof(rt_scene_desc),
-   sizeof(rt_render_params), sizeof(rt_stats), offsetof(rt_scene_desc, ambient_radiance),
-   offsetof(rt_mesh, aabb), offsetof(rt_stats, kernel_ms));
+ printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_mesh),
+   sizeof(rt_scene_desc), sizeof(rt_render_params), sizeof(rt_stats), offsetof(rt_scene_desc, ambient_radiance),
+   offsetof(rt_mesh, aabb), offsetof(rt_stats, kernel_ms), sizeof(rt_mesh_source),
+   offsetof(rt_mesh_source, local_to_world), offsetof(rt_mesh_source, material), sizeof(rt_scene_info));
  return 0; }''')
     exe = tmp_path / "l"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(prog)], check=True)
@@ -70,7 +71,8 @@ int main(void){
     a = _rt_pkg.load().abi
     want = [C.sizeof(a.rt_material), C.sizeof(a.rt_mesh), C.sizeof(a.rt_scene_desc), C.sizeof(a.rt_render_params),
             C.sizeof(a.rt_stats), a.rt_scene_desc.ambient_radiance.offset, a.rt_mesh.aabb.offset,
-            a.rt_stats.kernel_ms.offset]
+            a.rt_stats.kernel_ms.offset, C.sizeof(a.rt_mesh_source), a.rt_mesh_source.local_to_world.offset,
+            a.rt_mesh_source.material.offset, C.sizeof(a.rt_scene_info)]
     assert vals == want
 
 

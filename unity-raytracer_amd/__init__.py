@@ -6,6 +6,6 @@ hyphen, so it is loaded under the module name ``unity_raytracer_amd``).
 """
 from . import abi, bands, scene, scenes, raytracing  # noqa: F401
 from .abi import load_library, RtError  # noqa: F401
-from .scene import Scene, Mesh, MaterialData, TriangleData, SphereData  # noqa: F401
+from .scene import Scene, Mesh, MeshSource, MaterialData, TriangleData, SphereData  # noqa: F401
 from .scenes import CameraData, ImagePlane, Frame, make  # noqa: F401
 from .raytracing import Context, RayTracingSetup, params_struct, frame_params  # noqa: F401

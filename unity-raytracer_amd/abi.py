@@ -144,6 +144,17 @@ class rt_stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class rt_mesh_source(C.Structure):
+    _fields_ = [
+        ("vertices", C.c_void_p),
+        ("vertex_count", C.c_int32),
+        ("indices", C.c_void_p),
+        ("index_count", C.c_int32),
+        ("local_to_world", C.c_float * 16),
+        ("material", rt_material),
+    ]
+
+
 class rt_scene_info(C.Structure):
     _fields_ = [
         ("build", C.c_int32),
@@ -177,6 +188,8 @@ SIGNATURES = {
     "rt_set_scene": (C.c_int, [_P, C.POINTER(rt_scene_desc)]),
     "rt_set_scene_ex": (C.c_int, [_P, C.POINTER(rt_scene_desc), C.c_int32]),
     "rt_get_scene_info": (C.c_int, [_P, C.POINTER(rt_scene_info)]),
+    "rt_set_scene_source": (C.c_int, [_P, C.POINTER(rt_scene_desc), _P, C.c_int32]),
+    "rt_update_mesh_transforms": (C.c_int, [_P, _P, C.c_int32]),
     "rt_render": (C.c_int, [_P, C.POINTER(rt_camera), C.POINTER(rt_image_plane),
                             C.POINTER(rt_render_params), _P, C.POINTER(rt_stats)]),
     "rt_render_device": (C.c_int, [_P, C.POINTER(rt_camera), C.POINTER(rt_image_plane),

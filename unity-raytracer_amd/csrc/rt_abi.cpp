@@ -24,6 +24,7 @@
 #include "bvh.h"
 #include "kernels.h"
 #include "lbvh.h"
+#include "scene_xform.h"
 #include "rt_device.h"
 #include "rt_math.h"
 
@@ -38,15 +39,27 @@ struct GrowBuf {
 struct LbvhBufs {
     GrowBuf meshes, mesh_tris, mesh_normals, spheres, sphere_mat, loose_tris, loose_normals, loose_mat;
     GrowBuf nodes, nodes4, tris, sphs, shade, scratch;
+    // device mesh extraction (scene_xform.hip): resident sources + matrices
+    GrowBuf src_meshes, src_local, src_indices, src_matrices, src_world, src_aabbs;
     void release() {
         GrowBuf *all[] = {&meshes, &mesh_tris, &mesh_normals, &spheres, &sphere_mat, &loose_tris, &loose_normals,
-                          &loose_mat, &nodes, &nodes4, &tris, &sphs, &shade, &scratch};
+                          &loose_mat, &nodes, &nodes4, &tris, &sphs, &shade, &scratch, &src_meshes, &src_local,
+                          &src_indices, &src_matrices, &src_world, &src_aabbs};
         for (GrowBuf *b : all) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
         }
     }
+};
+
+// State kept by rt_set_scene_source for rt_update_mesh_transforms.
+struct SourceState {
+    bool active = false;
+    int mesh_count = 0, vertex_total = 0, tri_total = 0;
+    float rest_lo[3], rest_hi[3];  // Scene.CalculateAABB over loose triangles and spheres
+    rtl::LbvhInput in{};           // device inputs of the last build
+    bool wide = true;
 };
 
 struct DeviceArrays {
@@ -82,6 +95,7 @@ struct rt_ctx {
     int last_bvh_depth = 0;
     rt_scene_info info{};
     LbvhBufs lb;
+    SourceState src;
 };
 
 namespace {
@@ -372,11 +386,87 @@ hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
     return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
 }
 
+// Scene.CalculateAABB (Scene.cs:17-41) with Unity min/max semantics:
+// mesh AABBs, then loose triangle vertices, then sphere boxes.
+void scene_aabb(const rt_scene_desc *sc, rtm::f3 &smin_out, rtm::f3 &smax_out) {
+    const int NS = sc->sphere_count, NL = sc->triangle_count;
+    rtm::f3 smin = rtm::mk(FLT_MAX, FLT_MAX, FLT_MAX), smax = rtm::mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+    auto enc_box = [&](rtm::f3 lo, rtm::f3 hi) {  // AABB.Encapsulate(AABB): min(Min, other.Min)
+        smin = rtm::mk(rtm::umin(smin.x, lo.x), rtm::umin(smin.y, lo.y), rtm::umin(smin.z, lo.z));
+        smax = rtm::mk(rtm::umax(smax.x, hi.x), rtm::umax(smax.y, hi.y), rtm::umax(smax.z, hi.z));
+    };
+    auto enc_pt = [&](rtm::f3 p) {  // AABB.Encapsulate(float3): min(point, Min)
+        smin = rtm::mk(rtm::umin(p.x, smin.x), rtm::umin(p.y, smin.y), rtm::umin(p.z, smin.z));
+        smax = rtm::mk(rtm::umax(p.x, smax.x), rtm::umax(p.y, smax.y), rtm::umax(p.z, smax.z));
+    };
+    for (int m = 0; m < sc->mesh_count; ++m) enc_box(F3(sc->meshes[m].aabb.min), F3(sc->meshes[m].aabb.max));
+    for (int i = 0; i < NL; ++i) {
+        enc_pt(F3(sc->triangles[i].vertex0));
+        enc_pt(F3(sc->triangles[i].vertex1));
+        enc_pt(F3(sc->triangles[i].vertex2));
+    }
+    for (int i = 0; i < NS; ++i) {  // Sphere.AABB, Sphere.cs:17-22
+        const rtm::f3 c = F3(sc->spheres[i].center);
+        const float r = sqrtf(sc->spheres[i].radius_squared);
+        enc_box(rtm::mk(c.x - r, c.y - r, c.z - r), rtm::mk(c.x + r, c.y + r, c.z + r));
+    }
+    smin_out = smin;
+    smax_out = smax;
+}
+
+// Absolute node-box padding: 2^-13 of the scene's coordinate scale.
+float pad_abs_of(rtm::f3 smin, rtm::f3 smax) {
+    float scale = 1.0f;
+    for (float v : {smin.x, smin.y, smin.z, smax.x, smax.y, smax.z})
+        if (std::isfinite(v)) scale = std::max(scale, std::fabs(v));
+    return scale * 0x1p-13f;
+}
+
+// Runs the device build on inputs already resident (ctx->lb) and points the
+// scene at its output.
+int run_lbvh(rt_ctx *ctx, const rtl::LbvhInput &in, bool wide, rtd::SceneDev &S, int &nodes_count) {
+    LbvhBufs &B = ctx->lb;
+    const int P = in.mt + in.ns + in.nl;
+    rtl::LbvhOutput out{};
+    out.nodes = (rtd::BvhNode *)B.nodes.p;
+    out.nodes4 = wide ? (rtd::BvhNode4 *)B.nodes4.p : nullptr;
+    out.tris = (rtd::TriRec *)B.tris.p;
+    out.sphs = (rtd::SphRec *)B.sphs.p;
+    out.shade = (float4 *)B.shade.p;
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_OR_FAIL(ctx, rtl::build_lbvh_gpu(in, out, B.scratch.p, B.scratch.cap, ctx->stream));
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    float ms = 0.0f;
+    HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->info.build_ms += ms;
+    int binfo[2] = {0, 0};
+    HIP_OR_FAIL(ctx, hipMemcpy(binfo, rtl::lbvh_info_ptr(B.scratch.p, P), sizeof(binfo), hipMemcpyDeviceToHost));
+    ctx->last_bvh_depth = binfo[0];
+    // traversal stack: one entry per 2-wide level, three per 4-wide level
+    const int need = wide ? 3 * ((binfo[0] + 1) / 2 + 1) : binfo[0] + 1;
+    if (need > rtd::kStackTotal)
+        return fail(ctx, RT_E_SCENE, "LBVH depth %d exceeds the traversal stack; use RT_BUILD_SAH_HOST", binfo[0]);
+    S.nodes = (const rtd::BvhNode *)B.nodes.p;
+    S.nodes4 = wide ? (const rtd::BvhNode4 *)B.nodes4.p : nullptr;
+    S.tris = (const rtd::TriRec *)B.tris.p;
+    S.sphs = (const rtd::SphRec *)B.sphs.p;
+    S.shade = (const float4 *)B.shade.p;
+    S.bvh4 = wide ? 1 : 0;
+    nodes_count = wide ? binfo[1] : std::max(1, P - 1);
+    ctx->src.in = in;
+    ctx->src.wide = wide;
+    return RT_OK;
+}
+
 // GPU LBVH path of rt_set_scene_ex: uploads the caller's arrays as they are
 // (no per-primitive host work beyond material ids) and builds on the device.
+// geom_on_device: the mesh triangles/normals were produced on the device
+// (rt_set_scene_source) and are already in ctx->lb.
 template <typename MatId>
 int set_scene_lbvh(rt_ctx *ctx, const rt_scene_desc *sc, int MT, int NS, int NL, rtm::f3 smin, rtm::f3 smax,
-                   float pad_abs, MatId &mat_id, bool wide, rtd::SceneDev &S, int &nodes_count) {
+                   float pad_abs, MatId &mat_id, bool wide, bool geom_on_device, rtd::SceneDev &S,
+                   int &nodes_count) {
     const int P = MT + NS + NL;
     std::vector<rtl::MeshDev> meshes((size_t)sc->mesh_count);
     for (int m = 0; m < sc->mesh_count; ++m) {
@@ -390,8 +480,10 @@ int set_scene_lbvh(rt_ctx *ctx, const rt_scene_desc *sc, int MT, int NS, int NL,
     for (int i = 0; i < NL; ++i) loose_mat[i] = mat_id(sc->triangle_materials[i]);
     LbvhBufs &B = ctx->lb;
     HIP_OR_FAIL(ctx, put(ctx, B.meshes, meshes.data(), meshes.size()));
-    HIP_OR_FAIL(ctx, put(ctx, B.mesh_tris, sc->mesh_triangles, (size_t)sc->mesh_triangle_total));
-    HIP_OR_FAIL(ctx, put(ctx, B.mesh_normals, sc->mesh_triangle_normals, (size_t)sc->mesh_triangle_total));
+    if (!geom_on_device) {
+        HIP_OR_FAIL(ctx, put(ctx, B.mesh_tris, sc->mesh_triangles, (size_t)sc->mesh_triangle_total));
+        HIP_OR_FAIL(ctx, put(ctx, B.mesh_normals, sc->mesh_triangle_normals, (size_t)sc->mesh_triangle_total));
+    }
     HIP_OR_FAIL(ctx, put(ctx, B.spheres, sc->spheres, (size_t)NS));
     HIP_OR_FAIL(ctx, put(ctx, B.sphere_mat, sph_mat.data(), sph_mat.size()));
     HIP_OR_FAIL(ctx, put(ctx, B.loose_tris, sc->triangles, (size_t)NL));
@@ -421,35 +513,40 @@ int set_scene_lbvh(rt_ctx *ctx, const rt_scene_desc *sc, int MT, int NS, int NL,
     in.scene_hi[0] = smax.x; in.scene_hi[1] = smax.y; in.scene_hi[2] = smax.z;
     in.pad_abs = pad_abs;
     in.key_bits = 62;
-    rtl::LbvhOutput out{};
-    out.nodes = (rtd::BvhNode *)B.nodes.p;
-    out.nodes4 = wide ? (rtd::BvhNode4 *)B.nodes4.p : nullptr;
-    out.tris = (rtd::TriRec *)B.tris.p;
-    out.sphs = (rtd::SphRec *)B.sphs.p;
-    out.shade = (float4 *)B.shade.p;
+    return run_lbvh(ctx, in, wide, S, nodes_count);
+}
+
+int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geom_on_device,
+                   std::chrono::steady_clock::time_point t_start);
+
+// Device mesh extraction from the resident sources (scene_xform.hip); returns
+// the exact per-mesh AABBs on the host (they feed Scene.CalculateAABB).
+int extract_meshes(rt_ctx *ctx, std::vector<rtd::MeshGate> &aabbs, float &ms) {
+    LbvhBufs &B = ctx->lb;
+    rtx::XformArgs a{};
+    a.mesh_count = ctx->src.mesh_count;
+    a.vertex_total = ctx->src.vertex_total;
+    a.tri_total = ctx->src.tri_total;
+    a.meshes = (const rtx::MeshSrcDev *)B.src_meshes.p;
+    a.local = (const float *)B.src_local.p;
+    a.indices = (const int *)B.src_indices.p;
+    a.matrices = (const float *)B.src_matrices.p;
+    a.world = (float *)B.src_world.p;
+    a.tris = (float *)B.mesh_tris.p;
+    a.normals = (float *)B.mesh_normals.p;
+    a.aabbs = (rtd::MeshGate *)B.src_aabbs.p;
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    HIP_OR_FAIL(ctx, rtl::build_lbvh_gpu(in, out, B.scratch.p, B.scratch.cap, ctx->stream));
+    HIP_OR_FAIL(ctx, rtx::transform_meshes(a, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    aabbs.resize((size_t)a.mesh_count);
+    if (a.mesh_count)
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(aabbs.data(), B.src_aabbs.p, sizeof(rtd::MeshGate) * aabbs.size(),
+                                        hipMemcpyDeviceToHost, ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
-    float ms = 0.0f;
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-    ctx->info.build_ms = ms;
-    int binfo[2] = {0, 0};
-    HIP_OR_FAIL(ctx, hipMemcpy(binfo, rtl::lbvh_info_ptr(B.scratch.p, P), sizeof(binfo), hipMemcpyDeviceToHost));
-    ctx->last_bvh_depth = binfo[0];
-    // traversal stack: one entry per 2-wide level, three per 4-wide level
-    const int need = wide ? 3 * ((binfo[0] + 1) / 2 + 1) : binfo[0] + 1;
-    if (need > rtd::kStackTotal)
-        return fail(ctx, RT_E_SCENE, "LBVH depth %d exceeds the traversal stack; use RT_BUILD_SAH_HOST", binfo[0]);
-    S.nodes = (const rtd::BvhNode *)B.nodes.p;
-    S.nodes4 = wide ? (const rtd::BvhNode4 *)B.nodes4.p : nullptr;
-    S.tris = (const rtd::TriRec *)B.tris.p;
-    S.sphs = (const rtd::SphRec *)B.sphs.p;
-    S.shade = (const float4 *)B.shade.p;
-    S.bvh4 = wide ? 1 : 0;
-    nodes_count = wide ? binfo[1] : std::max(1, P - 1);
     return RT_OK;
 }
+
 
 }  // namespace
 
@@ -523,7 +620,16 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) { return rt_set_scene_ex(
 
 int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
     if (!ctx) return RT_E_INVALID;
-    auto t_start = std::chrono::steady_clock::now();
+    ctx->src.active = false;
+    return set_scene_impl(ctx, sc, build, false, std::chrono::steady_clock::now());
+}
+
+}  // extern "C"
+
+namespace {
+
+int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geom_on_device,
+                   std::chrono::steady_clock::time_point t_start) {
     if (!sc) return fail(ctx, RT_E_INVALID, "scene is null");
     if (build != RT_BUILD_SAH_HOST && build != RT_BUILD_LBVH_GPU && build != RT_BUILD_LBVH_GPU_BVH2)
         return fail(ctx, RT_E_INVALID, "unknown build %d", build);
@@ -532,7 +638,7 @@ int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
         return fail(ctx, RT_E_INVALID, "negative count in scene");
     if ((sc->triangle_count && (!sc->triangles || !sc->triangle_normals || !sc->triangle_materials)) ||
         (sc->mesh_count && !sc->meshes) ||
-        (sc->mesh_triangle_total && (!sc->mesh_triangles || !sc->mesh_triangle_normals)) ||
+        (sc->mesh_triangle_total && !geom_on_device && (!sc->mesh_triangles || !sc->mesh_triangle_normals)) ||
         (sc->sphere_count && (!sc->spheres || !sc->sphere_materials)) ||
         (sc->point_light_count && !sc->point_lights))
         return fail(ctx, RT_E_INVALID, "null array with a non-zero count");
@@ -556,26 +662,8 @@ int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
     const int P = MT + NS + NL;
 
     // Scene.CalculateAABB (Scene.cs:17-41) with Unity min/max semantics.
-    rtm::f3 smin = rtm::mk(FLT_MAX, FLT_MAX, FLT_MAX), smax = rtm::mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
-    auto enc_box = [&](rtm::f3 lo, rtm::f3 hi) {  // AABB.Encapsulate(AABB): min(Min, other.Min)
-        smin = rtm::mk(rtm::umin(smin.x, lo.x), rtm::umin(smin.y, lo.y), rtm::umin(smin.z, lo.z));
-        smax = rtm::mk(rtm::umax(smax.x, hi.x), rtm::umax(smax.y, hi.y), rtm::umax(smax.z, hi.z));
-    };
-    auto enc_pt = [&](rtm::f3 p) {  // AABB.Encapsulate(float3): min(point, Min)
-        smin = rtm::mk(rtm::umin(p.x, smin.x), rtm::umin(p.y, smin.y), rtm::umin(p.z, smin.z));
-        smax = rtm::mk(rtm::umax(p.x, smax.x), rtm::umax(p.y, smax.y), rtm::umax(p.z, smax.z));
-    };
-    for (int m = 0; m < sc->mesh_count; ++m) enc_box(F3(sc->meshes[m].aabb.min), F3(sc->meshes[m].aabb.max));
-    for (int i = 0; i < NL; ++i) {
-        enc_pt(F3(sc->triangles[i].vertex0));
-        enc_pt(F3(sc->triangles[i].vertex1));
-        enc_pt(F3(sc->triangles[i].vertex2));
-    }
-    for (int i = 0; i < NS; ++i) {  // Sphere.AABB, Sphere.cs:17-22
-        const rtm::f3 c = F3(sc->spheres[i].center);
-        const float r = sqrtf(sc->spheres[i].radius_squared);
-        enc_box(rtm::mk(c.x - r, c.y - r, c.z - r), rtm::mk(c.x + r, c.y + r, c.z + r));
-    }
+    rtm::f3 smin, smax;
+    scene_aabb(sc, smin, smax);
 
     // Materials, deduplicated.
     std::map<rt_material, int, bool (*)(const rt_material &, const rt_material &)> mat_ids(mat_less);
@@ -588,10 +676,7 @@ int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
         mats.push_back(to_dev(m));
         return id;
     };
-    float scale = 1.0f;
-    for (float v : {smin.x, smin.y, smin.z, smax.x, smax.y, smax.z})
-        if (std::isfinite(v)) scale = std::max(scale, std::fabs(v));
-    const float pad_abs = scale * 0x1p-13f;
+    const float pad_abs = pad_abs_of(smin, smax);
 
     ctx->mesh_rank_first.assign((size_t)sc->mesh_count + 1, 0);
     {
@@ -619,7 +704,7 @@ int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
     int nodes_count = 0;
     if ((build == RT_BUILD_LBVH_GPU || build == RT_BUILD_LBVH_GPU_BVH2) && P > 0) {
         const int st = set_scene_lbvh(ctx, sc, MT, NS, NL, smin, smax, pad_abs, mat_id,
-                                      build == RT_BUILD_LBVH_GPU, S, nodes_count);
+                                      build == RT_BUILD_LBVH_GPU, geom_on_device, S, nodes_count);
         if (st) return st;
     } else {
         // Host binned-SAH build (bvh.cpp), collapsed to 4-wide nodes.
@@ -758,6 +843,145 @@ int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
     ctx->info.total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     ctx->has_scene = true;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count) {
+    if (!ctx) return RT_E_INVALID;
+    const auto t0 = std::chrono::steady_clock::now();
+    ctx->src.active = false;
+    if (!base) return fail(ctx, RT_E_INVALID, "base scene is null");
+    if (mesh_count < 0 || (mesh_count && !meshes)) return fail(ctx, RT_E_INVALID, "bad mesh source array");
+    if (base->mesh_count || base->mesh_triangle_total)
+        return fail(ctx, RT_E_INVALID, "the base scene of rt_set_scene_source must not carry meshes");
+    int64_t vt = 0, tt = 0;
+    for (int m = 0; m < mesh_count; ++m) {
+        const rt_mesh_source &M = meshes[m];
+        if (M.vertex_count < 0 || M.index_count < 0 || M.index_count % 3)
+            return fail(ctx, RT_E_SCENE, "mesh %d: vertex_count %d / index_count %d invalid", m, M.vertex_count,
+                        M.index_count);
+        if ((M.vertex_count && !M.vertices) || (M.index_count && !M.indices))
+            return fail(ctx, RT_E_INVALID, "mesh %d: null array with a non-zero count", m);
+        vt += M.vertex_count;
+        tt += M.index_count / 3;
+    }
+    if (vt > (1ll << 28) || tt > (1ll << rtd::kLeafFirstBits))
+        return fail(ctx, RT_E_SCENE, "too many mesh vertices / triangles");
+    std::vector<rtx::MeshSrcDev> md((size_t)mesh_count);
+    std::vector<float> local((size_t)vt * 3), mats((size_t)mesh_count * 16);
+    std::vector<int> idx((size_t)tt * 3);
+    {
+        int v = 0, t = 0;
+        for (int m = 0; m < mesh_count; ++m) {
+            const rt_mesh_source &M = meshes[m];
+            md[m] = {v, M.vertex_count, t, M.index_count / 3};
+            if (M.vertex_count) std::memcpy(&local[(size_t)v * 3], M.vertices, sizeof(rt_float3) * M.vertex_count);
+            std::memcpy(&mats[(size_t)m * 16], M.local_to_world, sizeof(float) * 16);
+            for (int i = 0; i < M.index_count; ++i) {
+                const int k = M.indices[i];
+                if (k < 0 || k >= M.vertex_count)
+                    return fail(ctx, RT_E_SCENE, "mesh %d: index %d = %d outside [0, %d)", m, i, k, M.vertex_count);
+                idx[(size_t)t * 3 + i] = v + k;
+            }
+            v += M.vertex_count;
+            t += M.index_count / 3;
+        }
+    }
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    LbvhBufs &B = ctx->lb;
+    HIP_OR_FAIL(ctx, put(ctx, B.src_meshes, md.data(), md.size()));
+    HIP_OR_FAIL(ctx, put(ctx, B.src_local, local.data(), local.size()));
+    HIP_OR_FAIL(ctx, put(ctx, B.src_indices, idx.data(), idx.size()));
+    HIP_OR_FAIL(ctx, put(ctx, B.src_matrices, mats.data(), mats.size()));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.src_world, sizeof(float) * 3 * (size_t)vt));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.src_aabbs, sizeof(rtd::MeshGate) * (size_t)mesh_count));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.mesh_tris, sizeof(rt_triangle) * (size_t)tt));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.mesh_normals, sizeof(rt_float3) * (size_t)tt));
+    ctx->src.mesh_count = mesh_count;
+    ctx->src.vertex_total = (int)vt;
+    ctx->src.tri_total = (int)tt;
+    std::vector<rtd::MeshGate> aabbs;
+    float xform_ms = 0.0f;
+    int st = extract_meshes(ctx, aabbs, xform_ms);
+    if (st) return st;
+    std::vector<rt_mesh> dm((size_t)mesh_count);
+    for (int m = 0; m < mesh_count; ++m) {
+        dm[m].first_triangle = md[m].tri_first;
+        dm[m].triangle_count = md[m].tri_count;
+        dm[m].material = meshes[m].material;
+        dm[m].aabb.min = {aabbs[m].lo.x, aabbs[m].lo.y, aabbs[m].lo.z};
+        dm[m].aabb.max = {aabbs[m].hi.x, aabbs[m].hi.y, aabbs[m].hi.z};
+    }
+    rt_scene_desc d = *base;
+    d.meshes = dm.data();
+    d.mesh_count = mesh_count;
+    d.mesh_triangles = nullptr;
+    d.mesh_triangle_normals = nullptr;
+    d.mesh_triangle_total = (int32_t)tt;
+    st = set_scene_impl(ctx, &d, RT_BUILD_LBVH_GPU, true, t0);
+    if (st) return st;
+    ctx->info.build_ms += xform_ms;
+    rt_scene_desc rest = *base;  // loose triangles and spheres only
+    rtm::f3 lo, hi;
+    scene_aabb(&rest, lo, hi);
+    ctx->src.rest_lo[0] = lo.x; ctx->src.rest_lo[1] = lo.y; ctx->src.rest_lo[2] = lo.z;
+    ctx->src.rest_hi[0] = hi.x; ctx->src.rest_hi[1] = hi.y; ctx->src.rest_hi[2] = hi.z;
+    ctx->src.active = true;
+    return RT_OK;
+}
+
+int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count) {
+    if (!ctx) return RT_E_INVALID;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!ctx->has_scene || !ctx->src.active)
+        return fail(ctx, RT_E_STATE, "rt_update_mesh_transforms needs a scene from rt_set_scene_source");
+    if (mesh_count != ctx->src.mesh_count || (mesh_count && !local_to_world))
+        return fail(ctx, RT_E_INVALID, "expected %d matrices, got %d", ctx->src.mesh_count, mesh_count);
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    LbvhBufs &B = ctx->lb;
+    HIP_OR_FAIL(ctx, put(ctx, B.src_matrices, local_to_world, (size_t)mesh_count * 16));
+    std::vector<rtd::MeshGate> aabbs;
+    float xform_ms = 0.0f;
+    int st = extract_meshes(ctx, aabbs, xform_ms);
+    if (st) return st;
+    // Scene.CalculateAABB: mesh AABBs, then the (unchanged) loose triangles and spheres
+    rtm::f3 smin = rtm::mk(FLT_MAX, FLT_MAX, FLT_MAX), smax = rtm::mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
+    auto enc_box = [&](float4 lo, float4 hi) {
+        smin = rtm::mk(rtm::umin(smin.x, lo.x), rtm::umin(smin.y, lo.y), rtm::umin(smin.z, lo.z));
+        smax = rtm::mk(rtm::umax(smax.x, hi.x), rtm::umax(smax.y, hi.y), rtm::umax(smax.z, hi.z));
+    };
+    for (const rtd::MeshGate &g : aabbs) enc_box(g.lo, g.hi);
+    enc_box(make_float4(ctx->src.rest_lo[0], ctx->src.rest_lo[1], ctx->src.rest_lo[2], 0.0f),
+            make_float4(ctx->src.rest_hi[0], ctx->src.rest_hi[1], ctx->src.rest_hi[2], 0.0f));
+    if (mesh_count)
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->arr.gates, aabbs.data(), sizeof(rtd::MeshGate) * aabbs.size(),
+                                        hipMemcpyHostToDevice, ctx->stream));
+    rtd::SceneDev &S = ctx->S;
+    ctx->info.build_ms = xform_ms;
+    const int P = ctx->src.in.mt + ctx->src.in.ns + ctx->src.in.nl;
+    if (P > 0) {
+        rtl::LbvhInput in = ctx->src.in;
+        in.scene_lo[0] = smin.x; in.scene_lo[1] = smin.y; in.scene_lo[2] = smin.z;
+        in.scene_hi[0] = smax.x; in.scene_hi[1] = smax.y; in.scene_hi[2] = smax.z;
+        in.pad_abs = pad_abs_of(smin, smax);
+        int nodes = 0;
+        st = run_lbvh(ctx, in, ctx->src.wide, S, nodes);
+        if (st) {
+            ctx->has_scene = false;
+            return st;
+        }
+        ctx->info.nodes = nodes;
+    }
+    S.scene_lo[0] = smin.x; S.scene_lo[1] = smin.y; S.scene_lo[2] = smin.z;
+    S.scene_hi[0] = smax.x; S.scene_hi[1] = smax.y; S.scene_hi[2] = smax.z;
+    ctx->info.total_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
 }
 

@@ -1,0 +1,43 @@
+// scene_xform.h — mesh extraction on the device.
+//
+// The reference re-extracts every mesh on every Update()
+// (RayTracingSetup.cs:120-128,159-169 → SceneMesh.Mesh, SceneMesh.cs:11-53):
+//   * every local vertex goes through localToWorldMatrix.MultiplyPoint3x4
+//     (m00*x + m01*y + m02*z + m03 per row, left to right, no FMA);
+//   * Mesh.AABB = Encapsulate over ALL transformed vertices (SceneMesh.cs:22-31);
+//   * triangles come from the index buffer in order; the mesh normal of each
+//     is -Triangle.Normal = -(v / length(v)), v = cross(v2 - v0, v1 - v0)
+//     (Triangle.cs:13-21, SceneMesh.cs:43).
+// Here the local vertices and index buffers stay resident in HBM and a frame
+// only uploads the mesh_count 4x4 matrices; the world-space triangles and
+// normals land directly in the LBVH builder's input arrays.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_device.h"
+
+namespace rtx {
+
+struct MeshSrcDev {
+    int vertex_first;  // into the concatenated local vertex array
+    int vertex_count;
+    int tri_first;     // geometry index of the mesh's first triangle
+    int tri_count;
+};
+
+struct XformArgs {
+    int mesh_count, vertex_total, tri_total;
+    const MeshSrcDev *meshes;  // mesh_count
+    const float *local;        // vertex_total x 3
+    const int *indices;        // tri_total x 3, global vertex indices (validated on the host)
+    const float *matrices;     // mesh_count x 16, row-major m[row * 4 + col]
+    float *world;              // vertex_total x 3 (scratch)
+    float *tris;               // tri_total x 9 (rt_triangle layout)
+    float *normals;            // tri_total x 3
+    rtd::MeshGate *aabbs;      // mesh_count: exact Mesh.AABB
+};
+
+hipError_t transform_meshes(const XformArgs &a, hipStream_t stream);
+
+}  // namespace rtx

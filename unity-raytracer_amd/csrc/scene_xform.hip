@@ -1,0 +1,117 @@
+// scene_xform.hip — device mesh extraction (see scene_xform.h).
+#include "scene_xform.h"
+
+#include <float.h>
+
+#include "rt_math.h"
+
+namespace rtx {
+namespace {
+
+using rtm::f3;
+using rtm::mk;
+
+constexpr int kThreads = 256;
+
+// last mesh whose first element is <= i (empty meshes share their
+// successor's start, so the owner is always the last such mesh)
+template <int FIELD>
+__device__ __forceinline__ int owner(const MeshSrcDev *m, int count, int i) {
+    int a = 0, b = count - 1;
+    while (a < b) {
+        const int c = (a + b + 1) >> 1;
+        const int first = FIELD == 0 ? m[c].vertex_first : m[c].tri_first;
+        if (first <= i) a = c; else b = c - 1;
+    }
+    return a;
+}
+
+// Matrix4x4.MultiplyPoint3x4 (UnityEngine; restated in scene.py
+// multiply_point3x4): per row ((m0*x + m1*y) + m2*z) + m3, unfused.
+__global__ void k_vertices(XformArgs a) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= a.vertex_total) return;
+    const int m = owner<0>(a.meshes, a.mesh_count, v);
+    const float *M = a.matrices + (size_t)m * 16;
+    const float x = a.local[3 * (size_t)v], y = a.local[3 * (size_t)v + 1], z = a.local[3 * (size_t)v + 2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) a.world[3 * (size_t)v + r] = ((M[4 * r] * x + M[4 * r + 1] * y) + M[4 * r + 2] * z) + M[4 * r + 3];
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = rtm::umin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = rtm::umax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Mesh.AABB: Min = float.MaxValue, Max = float.MinValue (= -FLT_MAX), then
+// Encapsulate(point) = min(point, Min) / max(point, Max) for every vertex
+// (AABB.cs:10-14).  One wave per mesh; a NaN coordinate never enters
+// (Unity's min(x, y) keeps y unless y is NaN or x < y), so the partial
+// results are NaN-free and their combination order does not matter.
+__global__ void k_aabbs(XformArgs a) {
+    const int m = (blockIdx.x * blockDim.x + threadIdx.x) / rtd::kWaveSize;
+    const int lane = threadIdx.x % rtd::kWaveSize;
+    if (m >= a.mesh_count) return;
+    const MeshSrcDev M = a.meshes[m];
+    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int v = lane; v < M.vertex_count; v += rtd::kWaveSize) {
+        const float *p = a.world + 3 * (size_t)(M.vertex_first + v);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = rtm::umin(p[c], lo[c]);
+            hi[c] = rtm::umax(p[c], hi[c]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        lo[c] = wave_min(lo[c]);
+        hi[c] = wave_max(hi[c]);
+    }
+    if (lane == 0) {
+        a.aabbs[m].lo = make_float4(lo[0], lo[1], lo[2], 0.0f);
+        a.aabbs[m].hi = make_float4(hi[0], hi[1], hi[2], 0.0f);
+    }
+}
+
+// Triangles from the index buffer in order; mesh normal = -Triangle.Normal.
+__global__ void k_triangles(XformArgs a) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= a.tri_total) return;
+    const int *ix = a.indices + 3 * (size_t)t;
+    const float *w0 = a.world + 3 * (size_t)ix[0], *w1 = a.world + 3 * (size_t)ix[1],
+                *w2 = a.world + 3 * (size_t)ix[2];
+    const f3 v0 = mk(w0[0], w0[1], w0[2]), v1 = mk(w1[0], w1[1], w1[2]), v2 = mk(w2[0], w2[1], w2[2]);
+    float *o = a.tris + 9 * (size_t)t;
+    o[0] = v0.x; o[1] = v0.y; o[2] = v0.z;
+    o[3] = v1.x; o[4] = v1.y; o[5] = v1.z;
+    o[6] = v2.x; o[7] = v2.y; o[8] = v2.z;
+    const f3 v = rtm::cross(v2 - v0, v1 - v0);
+    const float len = sqrtf(rtm::dot(v, v));
+    float *n = a.normals + 3 * (size_t)t;
+    n[0] = -(v.x / len);
+    n[1] = -(v.y / len);
+    n[2] = -(v.z / len);
+}
+
+}  // namespace
+
+hipError_t transform_meshes(const XformArgs &a, hipStream_t stream) {
+    if (a.mesh_count <= 0) return hipSuccess;
+    if (a.vertex_total > 0)
+        hipLaunchKernelGGL(k_vertices, dim3((a.vertex_total + kThreads - 1) / kThreads), dim3(kThreads), 0, stream,
+                           a);
+    const int waves_per_block = kThreads / rtd::kWaveSize;
+    hipLaunchKernelGGL(k_aabbs, dim3((a.mesh_count + waves_per_block - 1) / waves_per_block), dim3(kThreads), 0,
+                       stream, a);
+    if (a.tri_total > 0)
+        hipLaunchKernelGGL(k_triangles, dim3((a.tri_total + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace rtx

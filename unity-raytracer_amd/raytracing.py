@@ -85,6 +85,23 @@ class Context:
         self._check(self.lib.rt_set_scene_ex(self.h, desc.ref(), int(build)))
         self._scene_desc = desc  # keep arrays alive for the duration of the call only; harmless
 
+    def set_scene_source(self, base: Scene, sources):
+        """Device-side mesh extraction + GPU BVH build: `base` holds loose
+        triangles, spheres and lights (no meshes); `sources` are MeshSource
+        objects (local vertices, index buffer, localToWorld, material)."""
+        from .scene import MeshSourceArray
+        if base.Meshes:
+            raise ValueError("base scene must not carry extracted meshes")
+        desc = base.to_desc()
+        arr = MeshSourceArray(list(sources))
+        self._check(self.lib.rt_set_scene_source(self.h, desc.ref(), arr.ptr(), arr.count))
+        self._scene_desc = desc
+
+    def update_mesh_transforms(self, local_to_world):
+        """Per-frame transform update (mesh_count x 4 x 4 f32, row-major)."""
+        m = np.ascontiguousarray(local_to_world, np.float32).reshape(-1, 16)
+        self._check(self.lib.rt_update_mesh_transforms(self.h, m.ctypes.data if m.size else None, len(m)))
+
     def scene_info(self) -> dict:
         info = abi.rt_scene_info()
         self._check(self.lib.rt_get_scene_info(self.h, C.byref(info)))

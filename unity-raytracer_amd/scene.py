@@ -179,6 +179,45 @@ class Mesh:
 
 
 @dataclass
+class MeshSource:
+    """A SceneMesh before extraction (SceneComponents/SceneMesh.cs:11-53):
+    MeshFilter.sharedMesh (local vertices + index buffer), the transform's
+    localToWorldMatrix and the MaterialData.  ``extract()`` is the host
+    restatement of the SceneMesh.Mesh getter; rt_set_scene_source runs the
+    same extraction on the device."""
+    Vertices: np.ndarray       # (V, 3) f32 local space
+    Indices: np.ndarray        # (3T,) int32
+    LocalToWorld: np.ndarray   # (4, 4) f32, row-major
+    MaterialData: MaterialData
+
+    def extract(self) -> "Mesh":
+        return Mesh.from_vertices(self.Vertices, self.Indices, self.MaterialData, self.LocalToWorld)
+
+
+class MeshSourceArray:
+    """ctypes rt_mesh_source[] over contiguous numpy arrays (kept alive here)."""
+
+    def __init__(self, sources: List[MeshSource]):
+        self.keep = []
+        self.arr = (abi.rt_mesh_source * max(1, len(sources)))()
+        self.count = len(sources)
+        for i, src in enumerate(sources):
+            v = np.ascontiguousarray(src.Vertices, f32).reshape(-1, 3)
+            ix = np.ascontiguousarray(src.Indices, np.int32).reshape(-1)
+            self.keep += [v, ix]
+            e = self.arr[i]
+            e.vertices = v.ctypes.data if v.size else None
+            e.vertex_count = len(v)
+            e.indices = ix.ctypes.data if ix.size else None
+            e.index_count = len(ix)
+            e.local_to_world[:] = [float(x) for x in np.asarray(src.LocalToWorld, f32).reshape(16)]
+            e.material = abi.rt_material.from_buffer_copy(src.MaterialData.record().tobytes())
+
+    def ptr(self):
+        return C.cast(self.arr, C.c_void_p)
+
+
+@dataclass
 class TriangleData:
     """Data/Objects/TriangleData.cs:8-13."""
     Triangles: np.ndarray = field(default_factory=lambda: np.zeros((0, 3, 3), f32))

@@ -21,7 +21,7 @@ from dataclasses import dataclass, replace
 
 import numpy as np
 
-from .scene import MaterialData, Mesh, Scene, quaternion_trs, triangle_normal
+from .scene import MaterialData, Mesh, MeshSource, Scene, quaternion_trs, triangle_normal
 
 f32 = np.float32
 SEED = 20250101
@@ -98,6 +98,22 @@ def unit_cube():
     return np.array(verts, f32), np.array(idx, np.int32)
 
 
+def demo_cube_source() -> MeshSource:
+    """The demo's Cube before extraction (RayTracing.unity:395-422)."""
+    cube_mat = MaterialData(DiffuseReflectance=(0, 1, 1))                               # Cube.prefab:100-118
+    verts, idx = unit_cube()
+    l2w = quaternion_trs((-24.7, 1.5497656e-6, 27.6),
+                         (-0.37513673, 0.13105033, 0.3026398, 0.8663183),
+                         (28.664, 10, 10))                                              # :395-422, Cube.prefab:31
+    return MeshSource(verts, idx, l2w, cube_mat)
+
+
+def without_meshes(sc: Scene) -> Scene:
+    """The non-mesh part of a scene (the base of rt_set_scene_source)."""
+    return Scene(TriangleData=sc.TriangleData, Meshes=[], SphereData=sc.SphereData,
+                 PointLights=sc.PointLights, AmbientLight=sc.AmbientLight)
+
+
 def demo_scene() -> Frame:
     """Assets/RayTracer/Demo-RayTracing/RayTracing.unity with prefab defaults.
 
@@ -117,12 +133,7 @@ def demo_scene() -> Frame:
                            MirrorReflectance=(1, 1, 1), SpecularReflectance=(0, 0, 0),
                            PhongExponent=20, IsMirror=False)
     sc.add_sphere((0, 0, 29.6), 20.0, sph_mat)                                          # :472-475, Sphere.prefab:31
-    cube_mat = MaterialData(DiffuseReflectance=(0, 1, 1))                               # Cube.prefab:100-118
-    verts, idx = unit_cube()
-    l2w = quaternion_trs((-24.7, 1.5497656e-6, 27.6),
-                         (-0.37513673, 0.13105033, 0.3026398, 0.8663183),
-                         (28.664, 10, 10))                                              # :395-422, Cube.prefab:31
-    sc.add_mesh(Mesh.from_vertices(verts, idx, cube_mat, l2w))
+    sc.add_mesh(demo_cube_source().extract())
     sc.add_point_light((5.79, 0, 0), 100000.0)                                          # :643-654, PointLight.prefab:47
     sc.AmbientLight = np.array([15, 15, 15], f32)                                       # AmbientLight.prefab:47-51
     return Frame("demo", sc, CameraData(), ImagePlane(50, 50, 10.0, 20.0, 10.0),
@@ -341,6 +352,59 @@ def hall_c5(n_boxes=20833, seed=SEED) -> Frame:
     sc.AmbientLight = np.array(AMBIENT, f32)
     return Frame("C5", sc, _camera_room(), ImagePlane(1920, 1080, 1.0, 0.8889, 0.5),
                  background=(0.0, 0.0, 0.0, 1.0), max_bounces=16, spp=64)
+
+
+def yaw_quaternion(yaw):
+    """Quaternion.Euler(0, yaw, 0) as (x, y, z, w) float32."""
+    h = np.asarray(yaw, np.float64) * 0.5
+    z = np.zeros_like(h)
+    return np.stack([z, np.sin(h), z, np.cos(h)], -1).astype(f32)
+
+
+def instanced_hall(n_boxes=20833, seed=SEED, res=(1920, 1080), spp=4, bounces=8):
+    """Animated variant of C5 for device-side extraction: n_boxes instances of
+    the unit cube, each a SceneMesh with its own Transform (position, yaw,
+    scale), inside the C2 room.  Returns (Frame with an empty-mesh base scene,
+    [MeshSource], matrices(t) -> (n, 4, 4)).  At time t every box spins about
+    y and bobs vertically, so every frame needs re-extraction and a rebuild
+    (UpdateScene, RayTracingSetup.cs:120-128)."""
+    rng = np.random.default_rng(seed)
+    sizes = rng.uniform(0.02, 0.2, (n_boxes, 3)).astype(f32)
+    pos = rng.uniform(-0.9, 0.9, (n_boxes, 3)).astype(f32)
+    yaw0 = rng.uniform(0.0, 2 * np.pi, n_boxes)
+    spin = rng.uniform(-2.0, 2.0, n_boxes)
+    phase = rng.uniform(0.0, 2 * np.pi, n_boxes)
+    mirror = rng.uniform(0.0, 1.0, n_boxes) < 0.1
+    near = np.linalg.norm(pos - np.asarray(LIGHT_POS, f32), axis=1) <= 0.35
+    pos[near, 1] = -0.5
+    verts, idx = unit_cube()
+
+    def matrices(t: float) -> np.ndarray:
+        q = yaw_quaternion(yaw0 + spin * t)
+        p = pos.copy()
+        p[:, 1] = (p[:, 1] + (0.05 * np.sin(phase + 3.0 * t))).astype(f32)
+        return np.stack([quaternion_trs(p[k], q[k], sizes[k]) for k in range(n_boxes)])
+
+    m0 = matrices(0.0)
+    sources = [MeshSource(verts, idx, m0[k], MIRROR if mirror[k] else BOX_MAT) for k in range(n_boxes)]
+    base = Scene()
+    add_room(base, with_lamp=True)
+    base.add_point_light(LIGHT_POS, LIGHT_I)
+    base.AmbientLight = np.array(AMBIENT, f32)
+    fr = Frame("C5i", base, _camera_room(), ImagePlane(res[0], res[1], 1.0, 0.8889, 0.5),
+               background=(0.0, 0.0, 0.0, 1.0), max_bounces=bounces, spp=spp)
+    return fr, sources, matrices
+
+
+def extracted(fr: Frame, sources, mats=None) -> Frame:
+    """Host extraction (SceneMesh.Mesh restated in scene.py) of `sources`
+    with optional replacement matrices: the reference-side scene."""
+    sc = Scene(TriangleData=fr.scene.TriangleData, Meshes=[], SphereData=fr.scene.SphereData,
+               PointLights=fr.scene.PointLights, AmbientLight=fr.scene.AmbientLight)
+    for k, src in enumerate(sources):
+        m = src.LocalToWorld if mats is None else mats[k]
+        sc.Meshes.append(Mesh.from_vertices(src.Vertices, src.Indices, src.MaterialData, m))
+    return fr.with_(scene=sc)
 
 
 def _boxes_vectorized(pos, sizes, yaw):
