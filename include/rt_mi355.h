@@ -143,6 +143,11 @@ typedef struct rt_render_params {
 #define RT_FLAG_COUNT_TESTS 1   /* fill rt_stats box/triangle/sphere counters (slower) */
 #define RT_FLAG_WAVEFRONT   2   /* per-level wavefront passes instead of the default megakernel */
 #define RT_FLAG_PACKET      4   /* wave-synchronous megakernel with per-wave packet traversal */
+/* Output pixel format (default: float RGBA = the reference's Color, 16 B).
+ * Encoding happens in the render kernel's final store, so the HBM write,
+ * the shard gather and the D2H copy shrink 4x / 2x. */
+#define RT_FLAG_OUT_RGBA8   8   /* Color32: round-half-even(clamp01(c) * 255), alpha 255; 4 B */
+#define RT_FLAG_OUT_RGBA16F 16  /* IEEE half RGBA (round to nearest even), alpha 1, unclamped; 8 B */
 
 /* Work counters and timings of the last render. */
 typedef struct rt_stats {
@@ -250,18 +255,22 @@ int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_so
 int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count);
 
 /* Render one frame: the MI355X replacement of CastPixelRays (:275-302).
- * out_rgba is a caller-owned HOST buffer of resolution_x*resolution_y*4
- * floats (row-major, y = 0 is the top row, alpha = 1), i.e. PixelColors.
- * When band_count > 1, only this shard's rows are rendered and out_rgba
- * receives the shard's compact buffer (rt_band_rows_local rows). */
+ * out_rgba is a caller-owned HOST buffer of resolution_x*resolution_y pixels
+ * of rt_pixel_bytes(flags) bytes — by default 4 floats (row-major, y = 0 is
+ * the top row, alpha = 1), i.e. PixelColors.  When band_count > 1, only this
+ * shard's rows are rendered and out_rgba receives the shard's compact
+ * buffer (rt_band_rows_local rows). */
 int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
-              const rt_render_params *params, float *out_rgba, rt_stats *stats);
+              const rt_render_params *params, void *out_rgba, rt_stats *stats);
+
+/* Bytes per output pixel for rt_render_params.flags: 16, 8 or 4. */
+int32_t rt_pixel_bytes(int32_t flags);
 
 /* Same as rt_render but the output stays in HBM: d_out_rgba is a DEVICE
  * pointer on the context's GPU of at least out_bytes bytes.  The call
  * returns after the frame is complete on the device. */
 int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
-                     const rt_render_params *params, float *d_out_rgba, size_t out_bytes,
+                     const rt_render_params *params, void *d_out_rgba, size_t out_bytes,
                      rt_stats *stats);
 
 /* Rows of the compact per-shard buffer for (resolution_y, band_index,
@@ -275,6 +284,11 @@ int32_t rt_band_rows_local(int32_t resolution_y, int32_t band_index, int32_t ban
 int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x,
                       int32_t resolution_y, int32_t band_count, int32_t band_rows,
                       float *d_image);
+
+/* rt_assemble_bands for any output format: pixel_bytes = rt_pixel_bytes(flags). */
+int rt_assemble_bands_ex(rt_ctx *ctx, const void *d_gathered, int32_t resolution_x,
+                         int32_t resolution_y, int32_t band_count, int32_t band_rows,
+                         int32_t pixel_bytes, void *d_image);
 
 /* Batch closest-hit query: Scene.IntersectRay (Scene.cs:43-122) for n host
  * rays; writes n host rt_hit records. */

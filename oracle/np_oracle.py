@@ -281,3 +281,23 @@ def render(fr, spp=None):
     out[:, :3] = total / f32(255)
     counts = {"primary_rays": cnt.primary, "shadow_rays": cnt.shadow, "reflection_rays": cnt.reflection}
     return out.reshape(ry, rx, 4), counts
+
+
+def encode_rgba8(color: np.ndarray) -> np.ndarray:
+    """Color -> Color32 (UnityEngine, closed source; restated from its public
+    behaviour): (byte)Mathf.Round(Mathf.Clamp01(c) * 255f) per channel, where
+    Mathf.Round is System.Math.Round (ties to even); alpha 255.  NaN -> 0
+    (C#'s unchecked NaN -> byte conversion is unspecified; the library
+    defines it as 0).  `color` is (..., 4) float32 Color."""
+    c = np.asarray(color, f32)[..., :3]
+    with np.errstate(invalid="ignore"):
+        v = np.rint(np.clip(c, f32(0), f32(1)) * f32(255))
+    v = np.where(np.isnan(c), f32(0), v).astype(np.uint8)
+    return np.concatenate([v, np.full(v.shape[:-1] + (1,), 255, np.uint8)], -1)
+
+
+def encode_rgba16f(color: np.ndarray) -> np.ndarray:
+    """IEEE binary16 RGBA (round to nearest even), unclamped, alpha 1."""
+    c = np.asarray(color, f32).copy()
+    c[..., 3] = 1.0
+    return c.astype(np.float16)

@@ -110,3 +110,18 @@ def test_spec_threshold(orc, rt):
         assert orc.spec_backfacing(float(x)) == bool(x < np.float32(T))
     for x in (-1.0, -0.5, -1e-7, -0.0, 0.0, 1e-7, 0.5, 1.0):
         assert orc.spec_backfacing(x) == bool(np.float32(x) < np.float32(T))
+
+
+def test_encode_rgba8_known_answers():
+    import np_oracle as npo
+    c = np.array([[0.5, 0.0, 1.0, 1.0], [-1.0, 2.0, np.nan, 1.0], [np.inf, -np.inf, 0.25, 1.0],
+                  [1.5 / 255, 2.5 / 255, 0.2 / 255, 1.0]], np.float32)
+    got = npo.encode_rgba8(c)
+    want = np.array([[128, 0, 255, 255], [0, 255, 0, 255], [255, 0, 64, 255], [2, 2, 0, 255]], np.uint8)
+    # 0.5*255 = 127.5 -> 128 (even); 0.25*255 = 63.75 -> 64; 1.5/255*255 rounds to 1.5 -> 2 (even),
+    # 2.5/255*255 -> 2.5 -> 2 (even)
+    assert np.float32(np.float32(1.5 / 255) * np.float32(255)) == np.float32(1.5)
+    assert np.float32(np.float32(2.5 / 255) * np.float32(255)) == np.float32(2.5)
+    assert np.array_equal(got, want)
+    h = npo.encode_rgba16f(c[:1])
+    assert h.dtype == np.float16 and h[0, 0] == np.float16(0.5) and h[0, 3] == 1

@@ -8,4 +8,4 @@ from . import abi, bands, scene, scenes, raytracing  # noqa: F401
 from .abi import load_library, RtError  # noqa: F401
 from .scene import Scene, Mesh, MeshSource, MaterialData, TriangleData, SphereData  # noqa: F401
 from .scenes import CameraData, ImagePlane, Frame, make  # noqa: F401
-from .raytracing import Context, RayTracingSetup, params_struct, frame_params  # noqa: F401
+from .raytracing import Context, RayTracingSetup, params_struct, frame_params, pixel_dtype, write_ppm  # noqa: F401

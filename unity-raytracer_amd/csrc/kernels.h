@@ -29,7 +29,7 @@ hipError_t launch_intersect(const rtd::SceneDev &S, const float *rays, int n, in
                             hipStream_t stream);
 
 // Row-order reassembly of block-cyclic shards gathered back to back.
-hipError_t launch_assemble(const float4 *gathered, int res_x, int res_y, int band_count,
-                           int band_rows, int local_rows, float4 *image, hipStream_t stream);
+hipError_t launch_assemble(const void *gathered, int res_x, int res_y, int band_count, int band_rows,
+                           int local_rows, int pixel_bytes, void *image, hipStream_t stream);
 
 }  // namespace rtk

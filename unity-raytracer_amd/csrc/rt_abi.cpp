@@ -257,7 +257,10 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.tiles_x = (F.res_x + tw - 1) / tw;
     const int tiles_y = (F.local_rows + th - 1) / th;
     F.num_tiles = F.res_x > 0 ? F.tiles_x * tiles_y : 0;
-    out_bytes = (size_t)F.local_rows * F.res_x * sizeof(float4);
+    const bool f8 = (prm->flags & RT_FLAG_OUT_RGBA8) != 0, f16 = (prm->flags & RT_FLAG_OUT_RGBA16F) != 0;
+    if (f8 && f16) return fail(ctx, RT_E_INVALID, "RT_FLAG_OUT_RGBA8 and RT_FLAG_OUT_RGBA16F are exclusive");
+    F.out_format = f8 ? rtd::kOutRGBA8 : (f16 ? rtd::kOutRGBA16F : rtd::kOutFloat4);
+    out_bytes = (size_t)F.local_rows * F.res_x * rt_pixel_bytes(prm->flags);
     return RT_OK;
 }
 
@@ -314,8 +317,8 @@ int prepare_wavefront(rt_ctx *ctx, const rtd::FrameDev &F, int &chunk_tiles, rtw
     return RT_OK;
 }
 
-int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, float4 *d_out, rt_stats *stats,
-              std::chrono::steady_clock::time_point t_start, float *host_out, size_t out_bytes) {
+int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *d_out, rt_stats *stats,
+              std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes) {
     F.out = d_out;
     F.counters = ctx->d_counters;
     const bool count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
@@ -998,7 +1001,7 @@ int32_t rt_band_rows_local(int32_t resolution_y, int32_t band_index, int32_t ban
 }
 
 int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane, const rt_render_params *params,
-              float *out_rgba, rt_stats *stats) {
+              void *out_rgba, rt_stats *stats) {
     if (!ctx) return RT_E_INVALID;
     auto t0 = std::chrono::steady_clock::now();
     rtd::FrameDev F;
@@ -1018,7 +1021,7 @@ int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
 }
 
 int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
-                     const rt_render_params *params, float *d_out_rgba, size_t out_bytes, rt_stats *stats) {
+                     const rt_render_params *params, void *d_out_rgba, size_t out_bytes, rt_stats *stats) {
     if (!ctx) return RT_E_INVALID;
     auto t0 = std::chrono::steady_clock::now();
     rtd::FrameDev F;
@@ -1029,19 +1032,29 @@ int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane 
     if (out_bytes < bytes)
         return fail(ctx, RT_E_INVALID, "output buffer %zu bytes < %zu required", out_bytes, bytes);
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    return run_frame(ctx, F, params, (float4 *)d_out_rgba, stats, t0, nullptr, 0);
+    return run_frame(ctx, F, params, d_out_rgba, stats, t0, nullptr, 0);
 }
 
 int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x, int32_t resolution_y,
                       int32_t band_count, int32_t band_rows, float *d_image) {
+    return rt_assemble_bands_ex(ctx, d_gathered, resolution_x, resolution_y, band_count, band_rows, 16, d_image);
+}
+
+int32_t rt_pixel_bytes(int32_t flags) {
+    return (flags & RT_FLAG_OUT_RGBA8) ? 4 : ((flags & RT_FLAG_OUT_RGBA16F) ? 8 : 16);
+}
+
+int rt_assemble_bands_ex(rt_ctx *ctx, const void *d_gathered, int32_t resolution_x, int32_t resolution_y,
+                         int32_t band_count, int32_t band_rows, int32_t pixel_bytes, void *d_image) {
     if (!ctx) return RT_E_INVALID;
-    if (!d_gathered || !d_image || resolution_x < 0 || resolution_y < 0 || band_count < 1)
+    if (!d_gathered || !d_image || resolution_x < 0 || resolution_y < 0 || band_count < 1 ||
+        (pixel_bytes != 4 && pixel_bytes != 8 && pixel_bytes != 16))
         return fail(ctx, RT_E_INVALID, "bad rt_assemble_bands arguments");
     if (band_rows <= 0) band_rows = 8;
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     const int local = band_local_rows(resolution_y, band_count, band_rows);
-    HIP_OR_FAIL(ctx, rtk::launch_assemble((const float4 *)d_gathered, resolution_x, resolution_y, band_count,
-                                          band_rows, local, (float4 *)d_image, ctx->stream));
+    HIP_OR_FAIL(ctx, rtk::launch_assemble(d_gathered, resolution_x, resolution_y, band_count, band_rows, local,
+                                          pixel_bytes, d_image, ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     return RT_OK;
 }

@@ -45,6 +45,11 @@ constexpr int kCounterWords = 8;
 constexpr int kLeafTri = 0;
 constexpr int kLeafSphere = 1;
 
+// Output pixel formats (rt_render_params.flags RT_FLAG_OUT_*).
+constexpr int kOutFloat4 = 0;   // Color, 16 B (the reference's Color[])
+constexpr int kOutRGBA8 = 1;    // Color32, 4 B
+constexpr int kOutRGBA16F = 2;  // half RGBA, 8 B
+
 struct alignas(16) BvhNode {
     float4 a;  // child0 lo.x, hi.x, lo.y, hi.y
     float4 b;  // child1 lo.x, hi.x, lo.y, hi.y
@@ -156,7 +161,8 @@ struct FrameDev {
     int local_rows;          // rows of the compact output buffer
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
-    float4 *out;             // local_rows x res_x RGBA
+    void *out;               // local_rows x res_x pixels in out_format
+    int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
 };
 

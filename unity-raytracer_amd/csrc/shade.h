@@ -95,6 +95,32 @@ __device__ __forceinline__ void primary_ray(const rtd::FrameDev &F, int px, int 
     d = rtm::normalize(pp - o);
 }
 
+// Color -> Color32 (UnityEngine, restated): (byte)Mathf.Round(Mathf.Clamp01(c)
+// * 255f); Mathf.Round rounds half to even (System.Math.Round).  A NaN
+// channel encodes as 0.
+__device__ __forceinline__ unsigned encode8(float c) {
+    if (!(c == c)) return 0u;
+    c = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
+    return (unsigned)rintf(c * 255.0f);
+}
+
+__device__ __forceinline__ unsigned half_bits(float c) {
+    return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)c);  // round to nearest even
+}
+
+// Final pixel store: v is the sample mean in Rgb.Value units (0..255);
+// Rgb.Color = Value / 255 (Rgb.cs:13), then the requested output format.
+__device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, rtm::f3 v) {
+    const float r = v.x / 255.0f, g = v.y / 255.0f, b = v.z / 255.0f;
+    if (F.out_format == rtd::kOutRGBA8) {
+        ((unsigned *)F.out)[idx] = encode8(r) | (encode8(g) << 8) | (encode8(b) << 16) | (255u << 24);
+    } else if (F.out_format == rtd::kOutRGBA16F) {
+        ((uint2 *)F.out)[idx] = make_uint2(half_bits(r) | (half_bits(g) << 16), half_bits(b) | (0x3C00u << 16));
+    } else {
+        ((float4 *)F.out)[idx] = make_float4(r, g, b, 1.0f);
+    }
+}
+
 // Slot (tile, lane) -> pixel; false for lanes outside the image/shard.
 __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int lane, int &px, int &ly, int &gy,
                                            int &s) {

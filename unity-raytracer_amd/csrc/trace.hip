@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kBlockThreads, RT_MK_MIN_WAVES) void render_kernel(
     if (active && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
-        F.out[(size_t)ly * F.res_x + px] = make_float4(v.x / 255.0f, v.y / 255.0f, v.z / 255.0f, 1.0f);  // Rgb.cs:13
+        rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
     }
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kBlockThreads) void render_packet_kernel(SceneDev S
     if (active && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
-        F.out[(size_t)ly * F.res_x + px] = make_float4(v.x / 255.0f, v.y / 255.0f, v.z / 255.0f, 1.0f);  // Rgb.cs:13
+        rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
     }
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
@@ -241,8 +241,9 @@ __global__ __launch_bounds__(kBlockThreads) void intersect_kernel(SceneDev S, co
     out[i] = make_int4(br, __float_as_int(bt), 0, 0);
 }
 
-__global__ void assemble_kernel(const float4 *gathered, int res_x, int res_y, int band_count, int band_rows,
-                                int local_rows, float4 *image) {
+template <typename Px>
+__global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int band_count, int band_rows,
+                                int local_rows, Px *image) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t total = (size_t)res_x * res_y;
     if (i >= total) return;
@@ -290,14 +291,24 @@ hipError_t launch_intersect(const SceneDev &S, const float *rays, int n, int4 *o
     return hipGetLastError();
 }
 
-hipError_t launch_assemble(const float4 *gathered, int res_x, int res_y, int band_count, int band_rows,
-                           int local_rows, float4 *image, hipStream_t stream) {
+hipError_t launch_assemble(const void *gathered, int res_x, int res_y, int band_count, int band_rows,
+                           int local_rows, int pixel_bytes, void *image, hipStream_t stream) {
     const size_t total = (size_t)res_x * res_y;
     if (total == 0) return hipSuccess;
     const int threads = 256;
     const unsigned blocks = (unsigned)((total + threads - 1) / threads);
-    hipLaunchKernelGGL(assemble_kernel, dim3(blocks), dim3(threads), 0, stream, gathered, res_x, res_y, band_count,
-                       band_rows, local_rows, image);
+    if (pixel_bytes == 16)
+        hipLaunchKernelGGL(assemble_kernel<float4>, dim3(blocks), dim3(threads), 0, stream, (const float4 *)gathered,
+                           res_x, res_y, band_count, band_rows, local_rows, (float4 *)image);
+    else if (pixel_bytes == 8)
+        hipLaunchKernelGGL(assemble_kernel<uint2>, dim3(blocks), dim3(threads), 0, stream, (const uint2 *)gathered,
+                           res_x, res_y, band_count, band_rows, local_rows, (uint2 *)image);
+    else if (pixel_bytes == 4)
+        hipLaunchKernelGGL(assemble_kernel<unsigned>, dim3(blocks), dim3(threads), 0, stream,
+                           (const unsigned *)gathered, res_x, res_y, band_count, band_rows, local_rows,
+                           (unsigned *)image);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kBlockThreads) void wf_resolve(FrameDev F, rtw::Arg
         f3 sum = xyz(A.col[e0]);
         for (int k = 1; k < F.spp; ++k) sum = sum + xyz(A.col[e0 + k]);
         if (F.spp > 1) sum = sum / (float)F.spp;
-        F.out[(size_t)ly * F.res_x + px] = make_float4(sum.x / 255.0f, sum.y / 255.0f, sum.z / 255.0f, 1.0f);
+        rts::store_pixel(F, (size_t)ly * F.res_x + px, sum);
     }
 }
 

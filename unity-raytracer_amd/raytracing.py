@@ -30,6 +30,25 @@ def plane_struct(p: ImagePlane) -> abi.rt_image_plane:
                               float(p.HalfHorizontalLength), float(p.HalfVerticalLength))
 
 
+def pixel_dtype(flags: int):
+    """numpy dtype of one output channel for rt_render_params.flags."""
+    if flags & abi.RT_FLAG_OUT_RGBA8:
+        return np.dtype(np.uint8)
+    if flags & abi.RT_FLAG_OUT_RGBA16F:
+        return np.dtype(np.float16)
+    return np.dtype(np.float32)
+
+
+def write_ppm(path: str, rgba8: np.ndarray):
+    """Binary PPM (P6) of an RGBA8 frame (alpha dropped); y = 0 is the top
+    row, as in PixelColors."""
+    img = np.ascontiguousarray(np.asarray(rgba8, np.uint8)[..., :3])
+    h, w = img.shape[:2]
+    with open(path, "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (w, h))
+        f.write(img.tobytes())
+
+
 def params_struct(background=(0, 0, 0, 1), max_bounces=0, spp=1, band_index=0, band_count=1,
                   band_rows=8, flags=0) -> abi.rt_render_params:
     p = abi.rt_render_params()
@@ -113,9 +132,10 @@ class Context:
         if params.band_count > 1:
             rows = self.lib.rt_band_rows_local(plane.ResolutionY, params.band_index,
                                                params.band_count, params.band_rows)
+        dtype = pixel_dtype(params.flags)
         if out is None:
-            out = np.empty((rows, plane.ResolutionX, 4), np.float32)
-        assert out.dtype == np.float32 and out.flags.c_contiguous and out.size >= rows * plane.ResolutionX * 4
+            out = np.empty((rows, plane.ResolutionX, 4), dtype)
+        assert out.dtype == dtype and out.flags.c_contiguous and out.size >= rows * plane.ResolutionX * 4
         stats = abi.rt_stats()
         cam, pl = camera_struct(camera), plane_struct(plane)
         self._check(self.lib.rt_render(self.h, C.byref(cam), C.byref(pl), C.byref(params),
@@ -131,9 +151,9 @@ class Context:
         return stats
 
     def assemble_bands(self, gathered_ptr: int, res_x: int, res_y: int, band_count: int,
-                       band_rows: int, image_ptr: int):
-        self._check(self.lib.rt_assemble_bands(self.h, C.c_void_p(gathered_ptr), res_x, res_y,
-                                               band_count, band_rows, C.c_void_p(image_ptr)))
+                       band_rows: int, image_ptr: int, pixel_bytes: int = 16):
+        self._check(self.lib.rt_assemble_bands_ex(self.h, C.c_void_p(gathered_ptr), res_x, res_y,
+                                                  band_count, band_rows, pixel_bytes, C.c_void_p(image_ptr)))
 
     def intersect_rays(self, rays: np.ndarray) -> np.ndarray:
         """Scene.IntersectRay (Scene.cs:43-122) for (N, 6) float32 rays;
