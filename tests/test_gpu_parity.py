@@ -31,7 +31,8 @@ def _check(img, ref, st, counts, name):
 
 
 # name -> (rt_render_params.flags, BVH builder: 0 host SAH, 1 GPU LBVH 4-wide, 2 GPU LBVH 2-wide)
-MODES = {"megakernel": (0, 0), "wavefront": (2, 0), "packet": (4, 0), "lbvh": (0, 1), "lbvh_wavefront": (2, 1),
+MODES = {"megakernel": (0, 0), "megakernel_count": (1, 0), "wavefront": (2, 0), "packet": (4, 0), "lbvh": (0, 1),
+         "lbvh_wavefront": (2, 1),
          "lbvh_packet": (4, 1), "lbvh2": (0, 2)}
 
 

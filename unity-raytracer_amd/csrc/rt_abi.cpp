@@ -321,6 +321,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
               std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes) {
     F.out = d_out;
     F.counters = ctx->d_counters;
+    F.tickets = (unsigned *)(ctx->d_counters + rtd::kCounterSlots * rtd::kCounterWords);
     const bool count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
     const bool packet = (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
     const bool wavefront = !packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
@@ -332,7 +333,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         if (st) return st;
     }
     const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
-    HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes, ctx->stream));
+    HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes + rtd::kTicketBytes, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     if (packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));
@@ -580,7 +581,8 @@ int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_counters, rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long)) !=
+        hipMalloc(&c->d_counters,
+                  rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long) + rtd::kTicketBytes) !=
             hipSuccess) {
         rt_destroy(c);
         return fail(nullptr, RT_E_HIP, "stream/event/counter allocation failed");

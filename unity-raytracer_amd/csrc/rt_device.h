@@ -41,6 +41,7 @@ constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;
 // serialise every wave's atomics (a single word saturates near 88 atomics/us).
 constexpr int kCounterSlots = 256;
 constexpr int kCounterWords = 8;
+constexpr int kTicketBytes = 256 * 64;  // tile tickets of the persistent megakernel (<= 256 shards x 64 B)
 
 constexpr int kLeafTri = 0;
 constexpr int kLeafSphere = 1;
@@ -164,6 +165,7 @@ struct FrameDev {
     void *out;               // local_rows x res_x pixels in out_format
     int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
+    unsigned *tickets;             // persistent megakernel tile tickets (shards x 64 B), zeroed per frame
 };
 
 }  // namespace rtd

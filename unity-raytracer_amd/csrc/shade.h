@@ -69,7 +69,11 @@ __device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &
         const f3 h = v / rtm::length(v);
         const float cnh = rtm::umax(0.0f, rtm::dot(s.n, h));
         // pow(float, float) = (float)System.Math.Pow((double)x, (double)y)
+#if RT_EXP_FLOAT_POW  // timing experiment only (not the reference's rounding): cost of the double pow
+        const float pw = powf(cnh, m.kd_phong.w);
+#else
         const float pw = (float)pow((double)cnh, (double)m.kd_phong.w);
+#endif
         spec = (mk(m.ks.x, m.ks.y, m.ks.z) * pw) * e;
     }
     return diffuse + spec;

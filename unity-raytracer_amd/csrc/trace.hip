@@ -10,6 +10,8 @@
 // FP32 — no MFMA.  Built with -ffp-contract=off and correctly rounded f32
 // divide/sqrt so every reference operation rounds exactly once.
 #include <float.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include <hip/hip_runtime.h>
@@ -31,8 +33,25 @@ namespace {
 // Shade with the mirror recursion unrolled into a loop; the recursion's
 // results are folded back to front so c0 + km0*(c1 + km1*(...)) rounds
 // exactly like the reference.
+// RT_MK_PACKET_SHADOW: the first level's shadow rays (all from one pixel tile
+// towards the same light, highly coherent) are traced as one wave packet
+// (packet.h, scalar node fetches); deeper levels per lane.  All lanes in a
+// loop iteration are at the same depth, so the choice is wave-uniform.
+#ifndef RT_MK_PACKET_SHADOW
+#define RT_MK_PACKET_SHADOW 1
+#endif
+// RT_MK_PACKET_PRIMARY: the same for the camera rays (closest hit).
+#ifndef RT_MK_PACKET_PRIMARY
+#define RT_MK_PACKET_PRIMARY 1
+#endif
+// Depths (0 = camera rays) traced as packets.
+#ifndef RT_MK_PACKET_DEPTHS
+#define RT_MK_PACKET_DEPTHS 1
+#endif
+
 template <bool COUNT>
-__device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st, Counts &cnt) {
+__device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
+                                         int *wstack, Counts &cnt) {
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
     int depth = 0;
@@ -42,7 +61,19 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         rtt::setup_ray(r, o, d);
         float bt;
         int br;
-        if (!rtt::traverse<false, COUNT>(S, r, 0.0f, 0.0f, bt, br, st, cnt)) {  // :310-311
+        bool hit;
+        // packets walk 4-wide nodes; the counting launch (bench.py's
+        // algorithmic-byte model) keeps the per-ray traversal's canonical counts
+        if (!COUNT && RT_MK_PACKET_PRIMARY && depth < RT_MK_PACKET_DEPTHS && S.bvh4) {
+            rtp::PacketLane P;
+            rtp::packet_trace<false, COUNT>(S, r, true, 0.0f, 0.0f, P, wstack, cnt);
+            bt = P.best_t;
+            br = P.best_rank;
+            hit = br >= 0;
+        } else {
+            hit = rtt::traverse<false, COUNT>(S, r, 0.0f, 0.0f, bt, br, st, cnt);
+        }
+        if (!hit) {  // :310-311
             term = rtt::ld3(F.bg255);
             break;
         }
@@ -56,7 +87,15 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
             rtt::setup_ray(rs, sr.o, sr.dir);
             float dt;
             int dr;
-            if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) continue;
+#if !RT_EXP_NO_SHADOW  // timing experiment only (wrong images): cost of the shadow queries
+            if (!COUNT && RT_MK_PACKET_SHADOW && depth < RT_MK_PACKET_DEPTHS && S.bvh4) {
+                rtp::PacketLane Q;
+                rtp::packet_trace<true, COUNT>(S, rs, true, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
+                if (Q.best_rank == 1) continue;
+            } else if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) {
+                continue;
+            }
+#endif
 #if RT_RELOAD
             // keep material/light out of registers across the traversal
             asm volatile("" ::: "memory");
@@ -84,27 +123,42 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
 #ifndef RT_MK_MIN_WAVES
 #define RT_MK_MIN_WAVES 4
 #endif
+// Waves per megakernel workgroup.  A workgroup's slot is recycled only when
+// all of its waves are done, and path lengths vary a lot between tiles, so
+// small workgroups keep the CUs fuller near the end of each wave "round".
+#ifndef RT_MK_WAVES
+#define RT_MK_WAVES 1
+#endif
+constexpr int kMkWaves = RT_MK_WAVES;
+constexpr int kMkThreads = kMkWaves * kWaveSize;
 
+// Persistent megakernel: the grid holds exactly the resident wave slots and
+// every wave loops over tiles: first its own id, then tickets from 8
+// sharded counters (shard c hands out tiles nw + c + kTicketShards*k; an exhausted shard
+// sends the wave to the next one), so no slot idles while tiles remain.
+#ifndef RT_MK_PERSIST
+#define RT_MK_PERSIST 0
+#endif
+#ifndef RT_TICKET_SHARDS
+#define RT_TICKET_SHARDS 64
+#endif
+constexpr int kTicketShards = RT_TICKET_SHARDS;
+constexpr int kTicketStride = 16;  // one 64-byte line per shard
+
+// One tile (a wave) of the megakernel: trace every sample, sum a pixel's
+// samples in row-major sample order ((s0 + s1) + s2) + ..., store.
 template <bool COUNT>
-__global__ __launch_bounds__(kBlockThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
-    __shared__ int stack_mem[kWavesPerBlock * kStackSize * kWaveSize];
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
-    const int tile = blockIdx.x * kWavesPerBlock + wave;
-    if (tile >= F.num_tiles) return;  // wave-uniform
+__device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
+                                            int *wstack, int tile, int lane, Counts &cnt) {
     int px, ly, gy, s;
     const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
-    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     f3 color = mk(0.0f, 0.0f, 0.0f);
     if (active) {
         f3 o, d;
         rts::primary_ray(F, px, gy, s, o, d);
-        cnt.primary = 1;
-        color = shade_path<COUNT>(S, F, o, d, st, cnt);
+        cnt.primary += 1;
+        color = shade_path<COUNT>(S, F, o, d, st, wstack, cnt);
     }
-    // Sum the pixel's samples in row-major sample order: ((s0 + s1) + s2) + ...
     f3 sum = color;
     for (int k = 1; k < F.spp; ++k) {
         const int src = lane + k;
@@ -114,6 +168,56 @@ __global__ __launch_bounds__(kBlockThreads, RT_MK_MIN_WAVES) void render_kernel(
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
         rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
+    __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
+    constexpr bool kPackets = RT_MK_PACKET_SHADOW || RT_MK_PACKET_PRIMARY;
+    __shared__ int wstack_mem[kPackets ? kMkWaves * rtp::kWaveStack : 1];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
+    int *const wstack = wstack_mem + (kPackets ? wave * rtp::kWaveStack : 0);
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    const int wid = blockIdx.x * kMkWaves + wave;
+    if (!RT_MK_PERSIST) {
+        if (wid >= F.num_tiles) return;  // wave-uniform
+        render_tile<COUNT>(S, F, st, wstack, wid, lane, cnt);
+    } else {
+        const int nw = gridDim.x * kMkWaves;
+        const int home = wid & (kTicketShards - 1);
+        unsigned *const home_ctr = F.tickets + home * kTicketStride;
+        // the next ticket is requested before the current tile is traced, so
+        // its atomic round trip overlaps the tile's first node fetches
+        unsigned q = 0;
+        if (lane == 0) q = atomicAdd(home_ctr, 1u);
+        int tile = wid;
+        while (tile < F.num_tiles) {  // wave-uniform
+            render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt);
+            int next = 0x7fffffff;
+            if (lane == 0) {
+                const long long cand = (long long)nw + home + (long long)kTicketShards * q;
+                if (cand < F.num_tiles) {
+                    next = (int)cand;
+                    q = atomicAdd(home_ctr, 1u);
+                } else {
+                    // home shard exhausted: take from the others (end of frame only)
+                    for (int k = 1; k < kTicketShards; ++k) {
+                        const int c = (home + k) & (kTicketShards - 1);
+                        const unsigned r = atomicAdd(F.tickets + c * kTicketStride, 1u);
+                        const long long cc = (long long)nw + c + (long long)kTicketShards * r;
+                        if (cc < F.num_tiles) {
+                            next = (int)cc;
+                            break;
+                        }
+                    }
+                }
+            }
+            tile = __builtin_amdgcn_readfirstlane(next);
+        }
     }
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
@@ -260,11 +364,26 @@ namespace rtk {
 
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
-    const int blocks = (F.num_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    int blocks = (F.num_tiles + kMkWaves - 1) / kMkWaves;
+    if (RT_MK_PERSIST) {
+        // resident workgroups: occupancy per CU x CUs (queried once)
+        static int resident = 0;
+        if (resident == 0) {
+            int dev = 0, cus = 0, per_cu = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e == hipSuccess)
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(
+                                                                    &render_kernel<false>), kMkThreads, 0);
+            if (e != hipSuccess) return e;
+            resident = std::max(1, cus * per_cu);
+        }
+        blocks = std::min(blocks, resident);
+    }
     if (count_tests)
-        hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kBlockThreads), 0, stream, S, F);
+        hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else
-        hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kBlockThreads), 0, stream, S, F);
+        hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     return hipGetLastError();
 }
 
