@@ -122,7 +122,8 @@ namespace RayTracer.Native
 
         public const int OK = 0;
         public const int BuildSahHost = 0, BuildLbvhGpu = 1, BuildLbvhGpuBvh2 = 2;
-        public const int FlagCountTests = 1, FlagWavefront = 2, FlagPacket = 4, FlagOutRgba8 = 8, FlagOutRgba16F = 16;
+        public const int FlagCountTests = 1, FlagWavefront = 2, FlagPacket = 4, FlagOutRgba8 = 8, FlagOutRgba16F = 16,
+                         FlagAsync = 32;
 
         [DllImport(Lib)] public static extern int rt_abi_version();
         [DllImport(Lib)] public static extern int rt_create(out IntPtr ctx, int numGpus);
@@ -145,6 +146,7 @@ namespace RayTracer.Native
                                                  ref RtRenderParams p, [Out] UnityEngine.Color32[] pixels,
                                                  out RtStats stats);
         [DllImport(Lib)] public static extern int rt_pixel_bytes(int flags);
+        [DllImport(Lib)] public static extern int rt_finish(IntPtr ctx, out RtStats stats);
         [DllImport(Lib)] public static extern int rt_render_device(IntPtr ctx, ref CameraData cam,
                                                                   ref RtImagePlane plane, ref RtRenderParams p,
                                                                   IntPtr devicePixels, UIntPtr outBytes,

@@ -148,6 +148,11 @@ typedef struct rt_render_params {
  * the shard gather and the D2H copy shrink 4x / 2x. */
 #define RT_FLAG_OUT_RGBA8   8   /* Color32: round-half-even(clamp01(c) * 255), alpha 255; 4 B */
 #define RT_FLAG_OUT_RGBA16F 16  /* IEEE half RGBA (round to nearest even), alpha 1, unclamped; 8 B */
+/* rt_render_device only: enqueue the frame on the context's stream and return
+ * without waiting (a frame loop that keeps the GPU fed).  The stats argument
+ * is zeroed; rt_finish waits and returns the counters and device time of all
+ * asynchronous frames since the previous rt_finish. */
+#define RT_FLAG_ASYNC       32
 
 /* Work counters and timings of the last render. */
 typedef struct rt_stats {
@@ -262,6 +267,11 @@ int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t 
  * buffer (rt_band_rows_local rows). */
 int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
               const rt_render_params *params, void *out_rgba, rt_stats *stats);
+
+/* Waits for the asynchronous frames (RT_FLAG_ASYNC) and returns their summed
+ * counters; kernel_ms is their summed device time, total_ms the wall time
+ * since the first of them was enqueued. */
+int rt_finish(rt_ctx *ctx, rt_stats *stats);
 
 /* Bytes per output pixel for rt_render_params.flags: 16, 8 or 4. */
 int32_t rt_pixel_bytes(int32_t flags);

@@ -214,3 +214,33 @@ def test_cpp_host_mirror_demo(tmp_path):
     g = np.load(os.path.join(root, "tests", "golden", "frames.npz"))
     assert np.array_equal(img[..., :3].view(np.uint32), g["demo"].view(np.uint32))
     assert np.all(img[..., 3] == 1.0)
+
+
+def test_async_frames(gpu_ctx, rt):
+    """RT_FLAG_ASYNC frames: same image as a synchronous frame, and rt_finish
+    returns the counters of all of them; a synchronous frame in between
+    settles the pending ones without losing their counts."""
+    import torch
+    fr = rt.make("C2").with_resolution(160, 90)
+    gpu_ctx.set_scene(fr.scene)
+    ref, sr = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+    out = torch.empty((90, 160, 4), dtype=torch.float32, device="cuda")
+    gpu_ctx.finish()
+    k = 5
+    for _ in range(k):
+        st = gpu_ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC),
+                                   out.data_ptr(), out.numel() * 4)
+        assert st.primary_rays == 0  # zeroed: counts come from rt_finish
+    tot = gpu_ctx.finish()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert (tot.primary_rays, tot.shadow_rays, tot.reflection_rays) == (k * sr.primary_rays, k * sr.shadow_rays,
+                                                                        k * sr.reflection_rays)
+    assert tot.kernel_ms > 0.0
+    # async, then sync, then finish: the async frame is still reported
+    gpu_ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC), out.data_ptr(),
+                          out.numel() * 4)
+    gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+    tot = gpu_ctx.finish()
+    assert tot.primary_rays == sr.primary_rays
+    with pytest.raises(rt.RtError):
+        gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC))

@@ -28,6 +28,7 @@ RT_FLAG_WAVEFRONT = 2
 RT_FLAG_PACKET = 4
 RT_FLAG_OUT_RGBA8 = 8
 RT_FLAG_OUT_RGBA16F = 16
+RT_FLAG_ASYNC = 32
 RT_BUILD_SAH_HOST = 0
 RT_BUILD_LBVH_GPU = 1
 RT_BUILD_LBVH_GPU_BVH2 = 2
@@ -199,6 +200,7 @@ SIGNATURES = {
     "rt_band_rows_local": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rt_assemble_bands": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_pixel_bytes": (C.c_int32, [C.c_int32]),
+    "rt_finish": (C.c_int, [_P, C.POINTER(rt_stats)]),
     "rt_assemble_bands_ex": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_intersect_rays": (C.c_int, [_P, _P, C.c_int32, _P]),
 }

@@ -86,6 +86,14 @@ struct rt_ctx {
     int4 *d_hits = nullptr;
     size_t rays_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // RT_FLAG_ASYNC frames: pending count, accumulated counters and device time
+    hipEvent_t ev_a0 = nullptr, ev_a1 = nullptr;
+    int async_frames = 0;
+    long long async_total_frames = 0;
+    unsigned long long async_acc[rtd::kCounterWords] = {0};
+    double async_ms = 0.0;
+    std::chrono::steady_clock::time_point async_t0;
+    bool async_t0_set = false;
     // wavefront queues (trace_wf.hip); pool_cap entries, shadow_cap shadow rays
     rtw::Counters *wf_ctr = nullptr;
     float4 *wf_ray_o = nullptr, *wf_ray_d = nullptr, *wf_col = nullptr, *wf_sh_o = nullptr, *wf_sh_d = nullptr;
@@ -317,6 +325,46 @@ int prepare_wavefront(rt_ctx *ctx, const rtd::FrameDev &F, int &chunk_tiles, rtw
     return RT_OK;
 }
 
+// Sums the sharded ray/test counters on the host (the stream must be idle).
+int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
+    const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
+    std::vector<unsigned long long> slots((size_t)rtd::kCounterSlots * rtd::kCounterWords);
+    HIP_OR_FAIL(ctx, hipMemcpy(slots.data(), ctx->d_counters, ctr_bytes, hipMemcpyDeviceToHost));
+    for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] = 0;
+    for (int sl = 0; sl < rtd::kCounterSlots; ++sl)
+        for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] += slots[(size_t)sl * rtd::kCounterWords + w];
+    return RT_OK;
+}
+
+void fill_stats(rt_stats *stats, const unsigned long long counts[rtd::kCounterWords], double kernel_ms,
+                double total_ms) {
+    stats->primary_rays = counts[0];
+    stats->shadow_rays = counts[1];
+    stats->reflection_rays = counts[2];
+    stats->box_tests = counts[3];
+    stats->triangle_tests = counts[4];
+    stats->sphere_tests = counts[5];
+    stats->shading_fetches = counts[6];
+    stats->kernel_ms = kernel_ms;
+    stats->total_ms = total_ms;
+}
+
+// Folds the counters and device time of pending RT_FLAG_ASYNC frames into the
+// context's accumulator (for rt_finish); waits for the stream.
+int settle_async(rt_ctx *ctx) {
+    if (ctx->async_frames == 0) return RT_OK;
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long counts[rtd::kCounterWords];
+    int st = read_counters(ctx, counts);
+    if (st) return st;
+    for (int w = 0; w < rtd::kCounterWords; ++w) ctx->async_acc[w] += counts[w];
+    float ms = 0.0f;
+    HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev_a0, ctx->ev_a1));
+    ctx->async_ms += ms;
+    ctx->async_frames = 0;
+    return RT_OK;
+}
+
 int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *d_out, rt_stats *stats,
               std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes) {
     F.out = d_out;
@@ -326,6 +374,12 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     const bool packet = (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
     const bool wavefront = !packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
     const bool mega = !packet && !wavefront;  // default
+    const bool async = (prm->flags & RT_FLAG_ASYNC) != 0;
+    if (async && host_out) return fail(ctx, RT_E_INVALID, "RT_FLAG_ASYNC needs a device output (rt_render_device)");
+    if (!async) {
+        int st = settle_async(ctx);
+        if (st) return st;
+    }
     int chunk_tiles = 0;
     rtw::Args A{};
     if (wavefront && F.num_tiles > 0) {
@@ -333,36 +387,40 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         if (st) return st;
     }
     const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
-    HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes + rtd::kTicketBytes, ctx->stream));
-    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    if (!async || ctx->async_frames == 0) {
+        // async frames share one set of counters until rt_finish / the next synchronous frame
+        HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes + rtd::kTicketBytes, ctx->stream));
+        HIP_OR_FAIL(ctx, hipEventRecord(async ? ctx->ev_a0 : ctx->ev0, ctx->stream));
+    } else if (mega && rtk::mega_uses_tickets()) {
+        HIP_OR_FAIL(ctx, hipMemsetAsync(F.tickets, 0, rtd::kTicketBytes, ctx->stream));
+    }
     if (packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));
     else if (mega)
         HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, count, ctx->stream));
     else if (wavefront && F.num_tiles > 0)
         HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, count, ctx->stream));
+    if (async) {
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_a1, ctx->stream));
+        if (ctx->async_frames++ == 0 && ctx->async_t0_set == false) {
+            ctx->async_t0 = t_start;
+            ctx->async_t0_set = true;
+        }
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    std::vector<unsigned long long> slots((size_t)rtd::kCounterSlots * rtd::kCounterWords);
-    HIP_OR_FAIL(ctx, hipMemcpyAsync(slots.data(), ctx->d_counters, ctr_bytes, hipMemcpyDeviceToHost, ctx->stream));
     if (host_out && out_bytes)
         HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
-    unsigned long long counts[rtd::kCounterWords] = {0};
-    for (int sl = 0; sl < rtd::kCounterSlots; ++sl)
-        for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] += slots[(size_t)sl * rtd::kCounterWords + w];
+    unsigned long long counts[rtd::kCounterWords];
+    int st = read_counters(ctx, counts);
+    if (st) return st;
     if (stats) {
         float ms = 0.0f;
         HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-        stats->primary_rays = counts[0];
-        stats->shadow_rays = counts[1];
-        stats->reflection_rays = counts[2];
-        stats->box_tests = counts[3];
-        stats->triangle_tests = counts[4];
-        stats->sphere_tests = counts[5];
-        stats->shading_fetches = counts[6];
-        stats->kernel_ms = ms;
-        stats->total_ms =
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        fill_stats(stats, counts, ms,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
     }
     return RT_OK;
 }
@@ -581,6 +639,7 @@ int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev_a0) != hipSuccess || hipEventCreate(&c->ev_a1) != hipSuccess ||
         hipMalloc(&c->d_counters,
                   rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long) + rtd::kTicketBytes) !=
             hipSuccess) {
@@ -605,6 +664,8 @@ void rt_destroy(rt_ctx *ctx) {
     if (ctx->d_rays) (void)hipFree(ctx->d_rays);
     if (ctx->d_hits) (void)hipFree(ctx->d_hits);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev_a0) (void)hipEventDestroy(ctx->ev_a0);
+    if (ctx->ev_a1) (void)hipEventDestroy(ctx->ev_a1);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -994,6 +1055,24 @@ int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info) {
     if (!ctx || !info) return RT_E_INVALID;
     if (!ctx->has_scene) return RT_E_STATE;
     *info = ctx->info;
+    return RT_OK;
+}
+
+int rt_finish(rt_ctx *ctx, rt_stats *stats) {
+    if (!ctx) return RT_E_INVALID;
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    const int st = settle_async(ctx);
+    if (st) return st;
+    if (stats) {
+        const double wall = ctx->async_t0_set ? std::chrono::duration<double, std::milli>(
+                                                    std::chrono::steady_clock::now() - ctx->async_t0)
+                                                    .count()
+                                              : 0.0;
+        fill_stats(stats, ctx->async_acc, ctx->async_ms, wall);
+    }
+    for (int w = 0; w < rtd::kCounterWords; ++w) ctx->async_acc[w] = 0;
+    ctx->async_ms = 0.0;
+    ctx->async_t0_set = false;
     return RT_OK;
 }
 

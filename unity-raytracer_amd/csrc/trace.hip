@@ -362,6 +362,8 @@ __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int ba
 
 namespace rtk {
 
+bool mega_uses_tickets() { return RT_MK_PERSIST != 0; }
+
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
     int blocks = (F.num_tiles + kMkWaves - 1) / kMkWaves;

@@ -150,6 +150,12 @@ class Context:
                                               C.c_void_p(dev_ptr), C.c_size_t(nbytes), C.byref(stats)))
         return stats
 
+    def finish(self) -> abi.rt_stats:
+        """Wait for RT_FLAG_ASYNC frames; their summed stats."""
+        stats = abi.rt_stats()
+        self._check(self.lib.rt_finish(self.h, C.byref(stats)))
+        return stats
+
     def assemble_bands(self, gathered_ptr: int, res_x: int, res_y: int, band_count: int,
                        band_rows: int, image_ptr: int, pixel_bytes: int = 16):
         self._check(self.lib.rt_assemble_bands_ex(self.h, C.c_void_p(gathered_ptr), res_x, res_y,
