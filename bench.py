@@ -118,39 +118,65 @@ def main():
     R = 8
     band_count = world
     local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if world > 1 else ry
-    out = torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda")
+    # N > 1: two frame buffers, so the gather of frame k (RCCL, async) runs
+    # while frame k+1 renders; rank 0 reassembles frame k once its gather is in
+    nbuf = 2 if world > 1 else 1
+    outs = [torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    out = outs[0]
     nbytes = out.numel() * 4
     mode_flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET}.get(args.mode, 0)
     params = rt.frame_params(fr, band_index=rank if world > 1 else 0, band_count=band_count, band_rows=R,
                              flags=mode_flags)
     if world > 1:
-        gathered = torch.empty((world, local_rows, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+        gath = [torch.empty((world, local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)] \
+            if rank == 0 else [None] * nbuf
         image = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
         if gloo:  # host staging buffers for the rehearsal backend
-            out_h = torch.empty((local_rows, rx, 4), dtype=torch.float32)
-            gathered_h = torch.empty((world, local_rows, rx, 4), dtype=torch.float32) if rank == 0 else None
+            outs_h = [torch.empty((local_rows, rx, 4), dtype=torch.float32) for _ in range(nbuf)]
+            gath_h = [torch.empty((world, local_rows, rx, 4), dtype=torch.float32) for _ in range(nbuf)] \
+                if rank == 0 else [None] * nbuf
+    pending = [None] * nbuf
 
-    def gather_shards():
-        """Shards -> rank 0 (RCCL gather over xGMI), then the HIP reassembly kernel."""
+    def begin_gather(b):
+        """Shard b -> rank 0 (RCCL gather over xGMI, async on the NCCL stream)."""
         if gloo:
-            out_h.copy_(out)
-            dist.gather(out_h, list(gathered_h.unbind(0)) if rank == 0 else None, dst=0)
-            if rank == 0:
-                gathered.copy_(gathered_h)
+            outs_h[b].copy_(outs[b])
+            src, dst_list = outs_h[b], (list(gath_h[b].unbind(0)) if rank == 0 else None)
         else:
-            dist.gather(out, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            src, dst_list = outs[b], (list(gath[b].unbind(0)) if rank == 0 else None)
+        pending[b] = dist.gather(src, dst_list, dst=0, async_op=True)
+
+    def finish_gather(b):
+        """Wait for buffer b's gather (stream-level wait for RCCL) and let
+        rank 0 put its rows back in order with the HIP reassembly kernel."""
+        w = pending[b]
+        if w is None:
+            return
+        w.wait()
+        pending[b] = None
         if rank == 0:
-            ctx.assemble_bands(gathered.data_ptr(), rx, ry, world, R, image.data_ptr())
+            if gloo:
+                gath[b].copy_(gath_h[b])
+            ctx.assemble_bands(gath[b].data_ptr(), rx, ry, world, R, image.data_ptr())
 
     # Frames are enqueued asynchronously (RT_FLAG_ASYNC): the host keeps the
     # stream fed and rt_finish returns the summed counters of the timed frames.
     aparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
                               flags=mode_flags | rt.abi.RT_FLAG_ASYNC)
+    frame_no = [0]
 
     def step():
-        ctx.render_device(fr.camera, fr.plane, aparams, out.data_ptr(), nbytes)
+        b = frame_no[0] % nbuf
+        finish_gather(b)  # buffer b is free again
+        ctx.render_device(fr.camera, fr.plane, aparams, outs[b].data_ptr(), nbytes)
         if world > 1:
-            gather_shards()
+            begin_gather(b)
+            finish_gather((b + nbuf - 1) % nbuf)  # the previous frame, gathered while this one rendered
+        frame_no[0] += 1
+
+    def drain():
+        for k in range(nbuf):
+            finish_gather((frame_no[0] + k) % nbuf)
 
     # counting launch (untimed): algorithmic work of this rank's frame
     cparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
@@ -160,6 +186,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    drain()
     ctx.finish()
     if world > 1:
         dist.barrier()
@@ -167,6 +194,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     st = ctx.finish()
     torch.cuda.synchronize()
     if world > 1:

@@ -192,6 +192,60 @@ __device__ __forceinline__ bool leaf(const rtd::SceneDev &S, const RayCtx &r, Tr
     return false;
 }
 
+// One triangle record against the lane's ray; true = any-hit occluder found.
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool tri_rec(const RayCtx &r, Trav &t, float d2, const rtd::TriRec &tr, Counts &cnt) {
+    float th;
+    if (COUNT) cnt.tri++;
+    if (rtm::ref_triangle(r.o, r.d, mk(tr.p0.x, tr.p0.y, tr.p0.z), mk(tr.p0.w, tr.p1.x, tr.p1.y),
+                          mk(tr.p1.z, tr.p1.w, tr.p2.x), th)) {
+        const int rank = __float_as_int(tr.p2.y);
+        if (ANY) {
+            if (th * th < d2) {
+                t.best_rank = 1;
+                return true;
+            }
+        } else if (th < t.best_t || (th == t.best_t && rank < t.best_rank)) {
+            t.best_t = th;
+            t.best_rank = rank;
+            t.tcull = th;
+        }
+    }
+    return false;
+}
+
+// Triangle leaf with every record fetched up front (indices clamped to the
+// leaf, so the loads are unconditional and issue back to back): one memory
+// latency per leaf instead of one per triangle; the gate comes from the
+// first record.
+#ifndef RT_LEAF_BATCH
+#define RT_LEAF_BATCH 0
+#endif
+template <bool ANY, bool COUNT>
+__device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
+                                                  int first, int count, Counts &cnt) {
+    const rtd::TriRec *b = S.tris + first;
+    const rtd::TriRec t0 = b[0];
+    const rtd::TriRec t1 = b[count > 1 ? 1 : 0];
+    const rtd::TriRec t2 = b[count > 2 ? 2 : 0];
+    const rtd::TriRec t3 = b[count > 3 ? 3 : 0];
+    const int gate = __float_as_int(t0.p2.z);
+    if (gate >= 0) {
+        if (gate != t.gate_cached) {
+            t.gate_cached = gate;
+            const rtd::MeshGate g = S.gates[gate];
+            t.gate_ok = rtm::ref_slab(r.o, r.inv, mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
+            if (COUNT) cnt.box++;
+        }
+        if (!t.gate_ok) return false;
+    }
+    if (tri_rec<ANY, COUNT>(r, t, d2, t0, cnt)) return true;
+    if (count > 1 && tri_rec<ANY, COUNT>(r, t, d2, t1, cnt)) return true;
+    if (count > 2 && tri_rec<ANY, COUNT>(r, t, d2, t2, cnt)) return true;
+    if (count > 3 && tri_rec<ANY, COUNT>(r, t, d2, t3, cnt)) return true;
+    return false;
+}
+
 #ifndef RT_PK_FMA
 #define RT_PK_FMA 0
 #endif
@@ -321,8 +375,12 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         const int first = v & ((1 << rtd::kLeafFirstBits) - 1);
         const int count = ((v >> rtd::kLeafFirstBits) & 3) + 1;
         const int kind = (v >> (rtd::kLeafFirstBits + 2)) & 1;
-        const int gate = kind == rtd::kLeafTri ? __float_as_int(S.tris[first].p2.z) : S.sphs[first].misc.y;
-        if (leaf<ANY, COUNT>(S, r, t, d2, first, count, kind, gate, cnt)) return true;
+        if (RT_LEAF_BATCH && kind == rtd::kLeafTri) {
+            if (leaf_tris_batched<ANY, COUNT>(S, r, t, d2, first, count, cnt)) return true;
+        } else {
+            const int gate = kind == rtd::kLeafTri ? __float_as_int(S.tris[first].p2.z) : S.sphs[first].misc.y;
+            if (leaf<ANY, COUNT>(S, r, t, d2, first, count, kind, gate, cnt)) return true;
+        }
     }
     return !pop(t, st);
 }
