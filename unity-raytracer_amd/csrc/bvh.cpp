@@ -9,8 +9,14 @@
 namespace rtb {
 namespace {
 
-constexpr int kBins = 32;
-constexpr float kTraversalCost = 1.0f;
+#ifndef RT_SAH_BINS
+#define RT_SAH_BINS 32
+#endif
+#ifndef RT_SAH_TRAVERSAL
+#define RT_SAH_TRAVERSAL 1.0f
+#endif
+constexpr int kBins = RT_SAH_BINS;
+constexpr float kTraversalCost = RT_SAH_TRAVERSAL;  // relative to one primitive test
 constexpr float kIntersectCost = 1.0f;
 
 struct Box {

@@ -197,7 +197,14 @@ rtd::DevMaterial to_dev(const rt_material &m) {
     d.ka_mirror = make_float4(m.ambient_reflectance.x, m.ambient_reflectance.y, m.ambient_reflectance.z,
                               m.is_mirror ? 1.0f : 0.0f);
     d.km = make_float4(m.mirror_reflectance.x, m.mirror_reflectance.y, m.mirror_reflectance.z, 0.0f);
-    d.ks = make_float4(m.specular_reflectance.x, m.specular_reflectance.y, m.specular_reflectance.z, 0.0f);
+    // ks.w = 1: the specular term is an exact signed zero for every hit, so
+    // the device may skip pow (shade.h light_term): SpecularReflectance is
+    // +-0 and PhongExponent in [0, 1e6] keeps pow(cnh <= 1 + 2^-22, n) finite
+    // and non-negative, hence (ks * pow) * E == (ks * 0) * E bit for bit.
+    const bool no_spec = m.specular_reflectance.x == 0.0f && m.specular_reflectance.y == 0.0f &&
+                         m.specular_reflectance.z == 0.0f && m.phong_exponent >= 0.0f && m.phong_exponent <= 1e6f;
+    d.ks = make_float4(m.specular_reflectance.x, m.specular_reflectance.y, m.specular_reflectance.z,
+                       no_spec ? 1.0f : 0.0f);
     return d;
 }
 

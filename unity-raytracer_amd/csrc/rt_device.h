@@ -112,7 +112,7 @@ struct alignas(16) DevMaterial {
     float4 kd_phong;   // DiffuseReflectance.xyz, PhongExponent
     float4 ka_mirror;  // AmbientReflectance.xyz, IsMirror (0/1 as float)
     float4 km;         // MirrorReflectance.xyz, -
-    float4 ks;         // SpecularReflectance.xyz, -
+    float4 ks;         // SpecularReflectance.xyz, 1 = specular term is always +-0 (pow skipped)
 };
 
 struct alignas(16) DevLight {

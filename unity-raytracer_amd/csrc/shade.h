@@ -55,6 +55,19 @@ __device__ __forceinline__ ShadowRay shadow_ray(const Surface &s, const rtd::Dev
     return r;
 }
 
+// (float)Math.Pow((double)x, (double)y).  Out of line by default: inlined,
+// the double-precision polynomial constants are hoisted to the kernel entry
+// and spilled to scratch for the whole frame (64 B per lane written, then
+// reloaded serially in every light loop).
+#ifndef RT_POW_NOINLINE
+#define RT_POW_NOINLINE 1
+#endif
+#if RT_POW_NOINLINE
+__device__ __attribute__((noinline)) float spec_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+#else
+__device__ __forceinline__ float spec_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+#endif
+
 // diffuseRgb + specularRgb of one unoccluded light (:350-355).
 __device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &s, const rtd::DevMaterial &m,
                                          const rtd::DevLight &L, const ShadowRay &sr) {
@@ -68,11 +81,13 @@ __device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &
         const f3 v = sr.dir + s.view;
         const f3 h = v / rtm::length(v);
         const float cnh = rtm::umax(0.0f, rtm::dot(s.n, h));
-        // pow(float, float) = (float)System.Math.Pow((double)x, (double)y)
+        // pow(float, float) = (float)System.Math.Pow((double)x, (double)y); a
+        // material whose specular term is always a signed zero skips it
+        // (ks.w, rt_abi.cpp to_dev): (ks * 0) * E has the same bits.
 #if RT_EXP_FLOAT_POW  // timing experiment only (not the reference's rounding): cost of the double pow
         const float pw = powf(cnh, m.kd_phong.w);
 #else
-        const float pw = (float)pow((double)cnh, (double)m.kd_phong.w);
+        const float pw = m.ks.w != 0.0f ? 0.0f : spec_pow(cnh, m.kd_phong.w);
 #endif
         spec = (mk(m.ks.x, m.ks.y, m.ks.z) * pw) * e;
     }

@@ -121,7 +121,7 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
 }
 
 #ifndef RT_MK_MIN_WAVES
-#define RT_MK_MIN_WAVES 4
+#define RT_MK_MIN_WAVES 5
 #endif
 // Waves per megakernel workgroup.  A workgroup's slot is recycled only when
 // all of its waves are done, and path lengths vary a lot between tiles, so

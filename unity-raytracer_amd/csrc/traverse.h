@@ -214,12 +214,13 @@ __device__ __forceinline__ bool tri_rec(const RayCtx &r, Trav &t, float d2, cons
     return false;
 }
 
-// Triangle leaf with every record fetched up front (indices clamped to the
+// Triangle leaf with the records fetched up front (indices clamped to the
 // leaf, so the loads are unconditional and issue back to back): one memory
-// latency per leaf instead of one per triangle; the gate comes from the
+// latency per leaf (RT_LEAF_BATCH 1: all four) or per pair of triangles
+// (RT_LEAF_BATCH 2) instead of one per triangle; the gate comes from the
 // first record.
 #ifndef RT_LEAF_BATCH
-#define RT_LEAF_BATCH 0
+#define RT_LEAF_BATCH 2
 #endif
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
@@ -227,8 +228,10 @@ __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const 
     const rtd::TriRec *b = S.tris + first;
     const rtd::TriRec t0 = b[0];
     const rtd::TriRec t1 = b[count > 1 ? 1 : 0];
+#if RT_LEAF_BATCH == 1
     const rtd::TriRec t2 = b[count > 2 ? 2 : 0];
     const rtd::TriRec t3 = b[count > 3 ? 3 : 0];
+#endif
     const int gate = __float_as_int(t0.p2.z);
     if (gate >= 0) {
         if (gate != t.gate_cached) {
@@ -241,8 +244,16 @@ __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const 
     }
     if (tri_rec<ANY, COUNT>(r, t, d2, t0, cnt)) return true;
     if (count > 1 && tri_rec<ANY, COUNT>(r, t, d2, t1, cnt)) return true;
-    if (count > 2 && tri_rec<ANY, COUNT>(r, t, d2, t2, cnt)) return true;
-    if (count > 3 && tri_rec<ANY, COUNT>(r, t, d2, t3, cnt)) return true;
+#if RT_LEAF_BATCH != 1  // pairs: the second pair is fetched together after the first
+    if (count > 2) {
+        const rtd::TriRec t2 = b[2];
+        const rtd::TriRec t3 = b[count > 3 ? 3 : 2];
+#endif
+        if (count > 2 && tri_rec<ANY, COUNT>(r, t, d2, t2, cnt)) return true;
+        if (count > 3 && tri_rec<ANY, COUNT>(r, t, d2, t3, cnt)) return true;
+#if RT_LEAF_BATCH != 1
+    }
+#endif
     return false;
 }
 
