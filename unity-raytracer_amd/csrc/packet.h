@@ -60,7 +60,7 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
     L.gate_cached = -1;
     L.gate_ok = false;
     if (COUNT && part) cnt.box++;
-    L.live = part && S.has_prims && rtm::ref_slab(r.o, r.inv, rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi));
+    L.live = part && S.has_prims && rtm::ref_slab(r.o, r.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi));
     if (__ballot(L.live) == 0) return;
     int node = 0;  // wave-uniform
     int sp = 0;    // wave-uniform

@@ -24,22 +24,49 @@ struct Counts {
     unsigned primary, shadow, reflection, box, tri, sph, shading;
 };
 
-struct RayCtx {
-    f3 o, d;  // exact ray (reference semantics)
-    f3 inv;   // rcp(dir) = 1.0f / dir, exact — the reference's AABB gates
-    f3 ninv;  // node-test inverse (zero components nudged, approximate rcp)
-    f3 noi;   // o * ninv
-};
+// RT_LEAN_RAY: keep only o, d and the node-test reciprocal in registers; the
+// exact 1/d (scene and mesh gates, rare) and o * ninv (once per node) are
+// recomputed where used — identical values, six fewer live registers across
+// every traversal.
+#ifndef RT_LEAN_RAY
+#define RT_LEAN_RAY 0
+#endif
 
 __device__ __forceinline__ float nudge(float v) { return fabsf(v) > 1e-20f ? v : copysignf(1e-20f, v); }
+
+struct RayCtx {
+    f3 o, d;  // exact ray (reference semantics)
+    f3 ninv;  // node-test inverse (zero components nudged, approximate rcp)
+#if !RT_LEAN_RAY
+    f3 inv_v, noi_v;
+#endif
+    // rcp(dir) = 1.0f / dir, exact — the reference's AABB gates
+    __device__ __forceinline__ f3 inv() const {
+#if RT_LEAN_RAY
+        return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+#else
+        return inv_v;
+#endif
+    }
+    // o * ninv
+    __device__ __forceinline__ f3 noi() const {
+#if RT_LEAN_RAY
+        return mk(o.x * ninv.x, o.y * ninv.y, o.z * ninv.z);
+#else
+        return noi_v;
+#endif
+    }
+};
 
 __device__ __forceinline__ void setup_ray(RayCtx &r, f3 o, f3 d) {
     r.o = o;
     r.d = d;
-    r.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     r.ninv = mk(__builtin_amdgcn_rcpf(nudge(d.x)), __builtin_amdgcn_rcpf(nudge(d.y)),
                 __builtin_amdgcn_rcpf(nudge(d.z)));
-    r.noi = mk(o.x * r.ninv.x, o.y * r.ninv.y, o.z * r.ninv.z);
+#if !RT_LEAN_RAY
+    r.inv_v = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.noi_v = mk(o.x * r.ninv.x, o.y * r.ninv.y, o.z * r.ninv.z);
+#endif
 }
 
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
@@ -64,12 +91,13 @@ __device__ __forceinline__ T cload(const T *p) {
 // Conservative slab test of both children of a node (padded boxes; FMA form).
 __device__ __forceinline__ void test_children(const float4 a, const float4 b, const float4 c, const RayCtx &r,
                                               float tcull, bool &h0, bool &h1, float &tn0, float &tn1) {
-    const float l0x = fmaf(a.x, r.ninv.x, -r.noi.x), u0x = fmaf(a.y, r.ninv.x, -r.noi.x);
-    const float l0y = fmaf(a.z, r.ninv.y, -r.noi.y), u0y = fmaf(a.w, r.ninv.y, -r.noi.y);
-    const float l0z = fmaf(c.x, r.ninv.z, -r.noi.z), u0z = fmaf(c.y, r.ninv.z, -r.noi.z);
-    const float l1x = fmaf(b.x, r.ninv.x, -r.noi.x), u1x = fmaf(b.y, r.ninv.x, -r.noi.x);
-    const float l1y = fmaf(b.z, r.ninv.y, -r.noi.y), u1y = fmaf(b.w, r.ninv.y, -r.noi.y);
-    const float l1z = fmaf(c.z, r.ninv.z, -r.noi.z), u1z = fmaf(c.w, r.ninv.z, -r.noi.z);
+    const f3 noi = r.noi();
+    const float l0x = fmaf(a.x, r.ninv.x, -noi.x), u0x = fmaf(a.y, r.ninv.x, -noi.x);
+    const float l0y = fmaf(a.z, r.ninv.y, -noi.y), u0y = fmaf(a.w, r.ninv.y, -noi.y);
+    const float l0z = fmaf(c.x, r.ninv.z, -noi.z), u0z = fmaf(c.y, r.ninv.z, -noi.z);
+    const float l1x = fmaf(b.x, r.ninv.x, -noi.x), u1x = fmaf(b.y, r.ninv.x, -noi.x);
+    const float l1y = fmaf(b.z, r.ninv.y, -noi.y), u1y = fmaf(b.w, r.ninv.y, -noi.y);
+    const float l1z = fmaf(c.z, r.ninv.z, -noi.z), u1z = fmaf(c.w, r.ninv.z, -noi.z);
     tn0 = fmaxf(fmaxf(fminf(l0x, u0x), fminf(l0y, u0y)), fmaxf(fminf(l0z, u0z), 0.0f));
     const float tf0 = fminf(fminf(fmaxf(l0x, u0x), fmaxf(l0y, u0y)), fminf(fmaxf(l0z, u0z), tcull));
     tn1 = fmaxf(fmaxf(fminf(l1x, u1x), fminf(l1y, u1y)), fmaxf(fminf(l1z, u1z), 0.0f));
@@ -100,11 +128,23 @@ struct Stack {
     int *ovf;
 };
 
+// RT_OVF_VOLATILE: volatile overflow accesses compile to system-coherent
+// (sc0 sc1) flat stores/loads that bypass the caches — every overflowing push
+// became an HBM write.  Plain private accesses stay in scratch (L1/L2).
+#ifndef RT_OVF_VOLATILE
+#define RT_OVF_VOLATILE 1
+#endif
+#if RT_OVF_VOLATILE
+typedef volatile int ovf_int;
+#else
+typedef int ovf_int;
+#endif
+
 __device__ __forceinline__ void push(Trav &t, const Stack &st, int v) {
     if (t.sp < rtd::kStackSize)
         st.lds[t.sp * kWaveSize] = v;
     else
-        ((volatile int *)st.ovf)[t.sp - rtd::kStackSize] = v;
+        ((ovf_int *)st.ovf)[t.sp - rtd::kStackSize] = v;
     ++t.sp;
 }
 
@@ -115,7 +155,7 @@ __device__ __forceinline__ bool pop(Trav &t, const Stack &st) {
     if (t.sp < rtd::kStackSize)
         t.node = st.lds[t.sp * kWaveSize];
     else
-        t.node = ((volatile int *)st.ovf)[t.sp - rtd::kStackSize];
+        t.node = ((ovf_int *)st.ovf)[t.sp - rtd::kStackSize];
     return true;
 }
 
@@ -132,7 +172,7 @@ __device__ __forceinline__ bool trav_begin(const rtd::SceneDev &S, const RayCtx 
     t.gate_cached = -1;
     t.gate_ok = false;
     if (COUNT) cnt.box++;
-    return S.has_prims && rtm::ref_slab(r.o, r.inv, ld3(S.scene_lo), ld3(S.scene_hi));
+    return S.has_prims && rtm::ref_slab(r.o, r.inv(), ld3(S.scene_lo), ld3(S.scene_hi));
 }
 
 // Primitive tests of one leaf (first, count, kind) behind the reference's
@@ -144,7 +184,7 @@ __device__ __forceinline__ bool leaf(const rtd::SceneDev &S, const RayCtx &r, Tr
         if (gate != t.gate_cached) {
             t.gate_cached = gate;
             const rtd::MeshGate g = S.gates[gate];
-            t.gate_ok = rtm::ref_slab(r.o, r.inv, mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
+            t.gate_ok = rtm::ref_slab(r.o, r.inv(), mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
             if (COUNT) cnt.box++;
         }
         if (!t.gate_ok) return false;
@@ -237,7 +277,7 @@ __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const 
         if (gate != t.gate_cached) {
             t.gate_cached = gate;
             const rtd::MeshGate g = S.gates[gate];
-            t.gate_ok = rtm::ref_slab(r.o, r.inv, mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
+            t.gate_ok = rtm::ref_slab(r.o, r.inv(), mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
             if (COUNT) cnt.box++;
         }
         if (!t.gate_ok) return false;
@@ -266,16 +306,17 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // or +inf when culled.
 __device__ __forceinline__ float child_key(float lx, float hx, float ly, float hy, float lz, float hz,
                                            const RayCtx &r, float tcull) {
+    const f3 noi = r.noi();
 #if RT_PK_FMA
     // packed FMA: both planes of an axis in one v_pk_fma_f32
-    const f2v px = __builtin_elementwise_fma((f2v){lx, hx}, (f2v){r.ninv.x, r.ninv.x}, (f2v){-r.noi.x, -r.noi.x});
-    const f2v py = __builtin_elementwise_fma((f2v){ly, hy}, (f2v){r.ninv.y, r.ninv.y}, (f2v){-r.noi.y, -r.noi.y});
-    const f2v pz = __builtin_elementwise_fma((f2v){lz, hz}, (f2v){r.ninv.z, r.ninv.z}, (f2v){-r.noi.z, -r.noi.z});
+    const f2v px = __builtin_elementwise_fma((f2v){lx, hx}, (f2v){r.ninv.x, r.ninv.x}, (f2v){-noi.x, -noi.x});
+    const f2v py = __builtin_elementwise_fma((f2v){ly, hy}, (f2v){r.ninv.y, r.ninv.y}, (f2v){-noi.y, -noi.y});
+    const f2v pz = __builtin_elementwise_fma((f2v){lz, hz}, (f2v){r.ninv.z, r.ninv.z}, (f2v){-noi.z, -noi.z});
     const float ax = px.x, bx = px.y, ay = py.x, by = py.y, az = pz.x, bz = pz.y;
 #else
-    const float ax = fmaf(lx, r.ninv.x, -r.noi.x), bx = fmaf(hx, r.ninv.x, -r.noi.x);
-    const float ay = fmaf(ly, r.ninv.y, -r.noi.y), by = fmaf(hy, r.ninv.y, -r.noi.y);
-    const float az = fmaf(lz, r.ninv.z, -r.noi.z), bz = fmaf(hz, r.ninv.z, -r.noi.z);
+    const float ax = fmaf(lx, r.ninv.x, -noi.x), bx = fmaf(hx, r.ninv.x, -noi.x);
+    const float ay = fmaf(ly, r.ninv.y, -noi.y), by = fmaf(hy, r.ninv.y, -noi.y);
+    const float az = fmaf(lz, r.ninv.z, -noi.z), bz = fmaf(hz, r.ninv.z, -noi.z);
 #endif
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tcull));
