@@ -10,8 +10,8 @@
 //   3. leaf-order primitive arrays + inline leaf refs (one primitive per leaf,
 //      so leaves are trivially homogeneous in kind and mesh gate);
 //   4. Karras hierarchy: n-1 internal nodes in parallel;
-//   5. bottom-up padded boxes, second arrival continues (agent-scope fences:
-//      per-XCD L2s are not coherent on MI355X);
+//   5. bottom-up padded boxes, second arrival continues (write-through sc1
+//      stores and sc1 loads: per-XCD L2s are not coherent on MI355X);
 //   6. node depths (climb to the root) -> even-depth flags -> scan;
 //   7. optional collapse to 4-wide nodes: every even-depth node adopts its
 //      grandchildren (leaf children keep their own slot).

@@ -204,21 +204,34 @@ __global__ void k_karras(int n, int empty_ref, const unsigned long long *k, cons
     if (i == 0) node_parent[0] = -1;
 }
 
-__device__ __forceinline__ void write_slot(rtd::BvhNode *nd, int side, float4 lo, float4 hi) {
-    float *a = side ? &nd->b.x : &nd->a.x;
-    a[0] = lo.x;
-    a[1] = hi.x;
-    a[2] = lo.y;
-    a[3] = hi.y;
-    float *c = &nd->c.x + 2 * side;
-    c[0] = lo.z;
-    c[1] = hi.z;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+// Agent-scope relaxed atomics on global memory compile to sc1 (write-through
+// / L2-bypassing) stores and loads: the hand-off between the two children of
+// a node needs no release/acquire fence (cdna_hip_programming.md G16; a
+// __threadfence() per level wrote back the whole L2 and cost 1.5 ms per
+// build at 250k primitives).
+__device__ __forceinline__ void st_sc1(float *p, float v) {
+    __hip_atomic_store((gu32 *)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __uint_as_float(__hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// 5. bottom-up boxes: each child writes its box into its parent's slot; the
-// second arrival (atomic counter) unions both slots and climbs.  Agent-scope
-// fences publish the slot before the count and make the sibling's slot
-// visible after it (per-XCD L2s and per-CU L1s are not coherent).
+__device__ __forceinline__ void write_slot(rtd::BvhNode *nd, int side, float4 lo, float4 hi) {
+    float *a = side ? &nd->b.x : &nd->a.x;
+    st_sc1(a + 0, lo.x);
+    st_sc1(a + 1, hi.x);
+    st_sc1(a + 2, lo.y);
+    st_sc1(a + 3, hi.y);
+    float *c = &nd->c.x + 2 * side;
+    st_sc1(c + 0, lo.z);
+    st_sc1(c + 1, hi.z);
+}
+
+// 5. bottom-up boxes: each child writes its box into its parent's slot
+// (sc1 stores, drained), then counts its arrival; the second arrival reads
+// the sibling's slot with sc1 loads, unions both and climbs.
 __global__ void k_bounds(int n, const float4 *slo, const float4 *shi, const int *leaf_parent,
                          const int *node_parent, rtd::BvhNode *nodes, int *flags) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -228,21 +241,14 @@ __global__ void k_bounds(int n, const float4 *slo, const float4 *shi, const int 
     while (ps >= 0) {
         const int p = ps >> 1, side = ps & 1;
         write_slot(&nodes[p], side, lo, hi);
-        __threadfence();
-        // release: the write-back must complete before the count is visible
-        // (MI355X_MICROARCH.md "Compiler hazard")
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(&flags[p], 1) == 0) return;
-        __threadfence();  // acquire: drop stale L1 copies of the sibling slot
-        const rtd::BvhNode nd = nodes[p];
-        float4 olo, ohi;
-        if (side) {  // sibling is slot 0
-            olo = make_float4(nd.a.x, nd.a.z, nd.c.x, 0.0f);
-            ohi = make_float4(nd.a.y, nd.a.w, nd.c.y, 0.0f);
-        } else {
-            olo = make_float4(nd.b.x, nd.b.z, nd.c.z, 0.0f);
-            ohi = make_float4(nd.b.y, nd.b.w, nd.c.w, 0.0f);
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot is visible before the count
+        if (__hip_atomic_fetch_add((__attribute__((address_space(1))) int *)&flags[p], 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == 0)
+            return;
+        const float *o = side ? &nodes[p].a.x : &nodes[p].b.x;  // the sibling's slot
+        const float *oc = &nodes[p].c.x + 2 * (1 - side);
+        const float4 olo = make_float4(ld_sc1(o + 0), ld_sc1(o + 2), ld_sc1(oc + 0), 0.0f);
+        const float4 ohi = make_float4(ld_sc1(o + 1), ld_sc1(o + 3), ld_sc1(oc + 1), 0.0f);
         lo = make_float4(fminf(lo.x, olo.x), fminf(lo.y, olo.y), fminf(lo.z, olo.z), 0.0f);
         hi = make_float4(fmaxf(hi.x, ohi.x), fmaxf(hi.y, ohi.y), fmaxf(hi.z, ohi.z), 0.0f);
         ps = node_parent[p];
