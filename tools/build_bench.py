@@ -19,11 +19,14 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--instanced", type=int, default=20833, help="instanced-hall boxes (0: skip)")
+    ap.add_argument("--variant", default="", help="library variant under unity-raytracer_amd/lib/variants/")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
     rt = _rt_pkg.load()
-    ctx = rt.Context()
+    lib = os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", a.variant, "librt_mi355.so") if a.variant \
+        else None
+    ctx = rt.Context(lib_path=lib)
     for name in a.configs:
         fr = rt.make(name)
         for build, label in ((0, "sah_host_bvh4"), (1, "lbvh_gpu_bvh4"), (2, "lbvh_gpu_bvh2")):
@@ -36,7 +39,7 @@ def main():
             for _ in range(a.frames):
                 _, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
                 times.append(st.kernel_ms)
-            rec = {"config": name, "build": label, "primitives": infos[-1]["primitives"],
+            rec = {"config": name, "variant": a.variant or "default", "build": label, "primitives": infos[-1]["primitives"],
                    "nodes": infos[-1]["nodes"],
                    "set_scene_ms_min": min(i["total_ms"] for i in infos),
                    "gpu_build_ms_min": min(i["build_ms"] for i in infos),

@@ -12,6 +12,10 @@ using rtm::f3;
 using rtm::mk;
 
 constexpr int kThreads = 256;
+#ifndef RT_LBVH_LEAF
+#define RT_LBVH_LEAF 4
+#endif
+constexpr int kLbvhLeaf = RT_LBVH_LEAF;  // max primitives per collapsed leaf (2-bit count field)
 
 inline int blocks_for(int n) { return (n + kThreads - 1) / kThreads; }
 
@@ -124,7 +128,7 @@ __global__ void k_kind(LbvhInput in, int n, const int *sorted_rank, int *is_sph)
 // 3. leaf-order primitive arrays, inline leaf refs, sorted boxes
 __global__ void k_leaves(LbvhInput in, LbvhOutput out, int n, const int *sorted_rank, const int *sph_idx,
                          const rtd::TriRec *tri_rank, const float4 *plo, const float4 *phi, float4 *slo, float4 *shi,
-                         int *leaf_ref) {
+                         int *leaf_ref, int *gate_pos) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) out.tris[in.mt + in.nl] = rtd::sentinel_tri();
     if (i >= n) return;
@@ -134,10 +138,13 @@ __global__ void k_leaves(LbvhInput in, LbvhOutput out, int n, const int *sorted_
     if (sph) {
         out.sphs[si] = *(const rtd::SphRec *)&tri_rank[r];
         leaf_ref[i] = rtd::encode_leaf(si, 1, rtd::kLeafSphere);
+        gate_pos[i] = -2;  // spheres: never grouped with triangles
     } else {
         const int ti = i - si;
-        out.tris[ti] = tri_rank[r];
+        const rtd::TriRec t = tri_rank[r];
+        out.tris[ti] = t;
         leaf_ref[i] = rtd::encode_leaf(ti, 1, rtd::kLeafTri);
+        gate_pos[i] = __float_as_int(t.p2.z);
     }
     slo[i] = plo[r];
     shi[i] = phi[r];
@@ -153,7 +160,7 @@ __device__ __forceinline__ int delta(const unsigned long long *k, int n, int i, 
 // 4. Karras 2012: internal node i covers a key range and splits it at the
 // highest differing bit; parents recorded as (node << 1 | side).
 __global__ void k_karras(int n, int empty_ref, const unsigned long long *k, const int *leaf_ref, const float4 *slo,
-                         const float4 *shi, rtd::BvhNode *nodes, int *leaf_parent, int *node_parent) {
+                         const float4 *shi, rtd::BvhNode *nodes, int *leaf_parent, int *node_parent, int2 *range) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (n == 1) {
         if (i == 0) {  // lone leaf beside an empty slot (+inf box, sentinel leaf)
@@ -185,6 +192,7 @@ __global__ void k_karras(int n, int empty_ref, const unsigned long long *k, cons
     } while (t > 1);
     const int gamma = i + s * d + (d < 0 ? -1 : 0);
     const int first = min(i, j), last = max(i, j);
+    range[i] = make_int2(first, last);
     int left, right;
     if (first == gamma) {
         left = leaf_ref[gamma];
@@ -255,14 +263,33 @@ __global__ void k_bounds(int n, const float4 *slo, const float4 *shi, const int 
     }
 }
 
-// 6. depth of every internal node (climb to the root; depths are small) and
-// the even-depth flag: even-depth nodes become 4-wide nodes.
-__global__ void k_depth(int n, const int *node_parent, int *even, int *max_depth) {
+// 6a. small homogeneous subtrees (<= 4 primitives of one kind and one mesh
+// gate, contiguous in leaf order) become one multi-primitive leaf in the
+// 4-wide tree — fewer traversal steps, like the host SAH build's leaves.
+__global__ void k_small(int n, const int2 *range, const int *gate_pos, int *small) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    const int2 r = range[i];
+    bool ok = i != 0 && r.y - r.x + 1 <= kLbvhLeaf;  // the root stays a node
+    if (ok) {
+        const int g = gate_pos[r.x];
+        for (int p = r.x + 1; p <= r.y; ++p) ok = ok && gate_pos[p] == g;
+    }
+    small[i] = ok ? 1 : 0;
+}
+
+// 6b. depth of every internal node (climb to the root; depths are small);
+// 4-wide nodes are the even-depth nodes not inside a collapsed subtree.
+__global__ void k_depth(int n, const int *node_parent, const int *small, int *even, int *max_depth) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n - 1) return;
     int d = 0;
-    for (int ps = node_parent[i]; ps >= 0; ps = node_parent[ps >> 1]) ++d;
-    even[i] = (d & 1) == 0;
+    bool inside = small[i] != 0;
+    for (int ps = node_parent[i]; ps >= 0; ps = node_parent[ps >> 1]) {
+        ++d;
+        inside = inside || small[ps >> 1] != 0;
+    }
+    even[i] = (d & 1) == 0 && !inside;
     // leaves sit one level below their parent
     atomicMax(max_depth, d + 1);
 }
@@ -280,17 +307,28 @@ __device__ __forceinline__ void read_slot(const rtd::BvhNode &nd, int side, floa
 // the sentinel leaf.  Child node refs are renumbered by the exclusive scan of
 // the even flags (the root stays 0).
 __global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, const int *even, const int *idx4,
+                           const int *small, const int2 *range, const int *sph_idx, const int *is_sph,
                            rtd::BvhNode4 *out, int *info) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) info[1] = n > 1 ? idx4[n - 2] + even[n - 2] : 1;  // 4-wide node count
     if (i >= (n > 1 ? n - 1 : 1) || (n > 1 && !even[i])) return;
+    // ref of an internal node c seen from a 4-wide node: a multi-primitive
+    // leaf when its subtree is small, else its 4-wide index
+    auto sub = [&](int c) {
+        if (!small[c]) return idx4[c];
+        const int2 r = range[c];
+        const int f = r.x;
+        const int sph = is_sph[f];
+        return rtd::encode_leaf(sph ? sph_idx[f] : f - sph_idx[f], r.y - r.x + 1,
+                                sph ? rtd::kLeafSphere : rtd::kLeafTri);
+    };
     float lo[3][4], hi[3][4];
     int ref[4];
     int k = 0;
     const rtd::BvhNode nd = nodes[i];
     const int ch[2] = {nd.d.x, nd.d.y};
     for (int s = 0; s < 2; ++s) {
-        if (ch[s] >= 0 && n > 1) {
+        if (ch[s] >= 0 && n > 1 && !small[ch[s]]) {
             const rtd::BvhNode cn = nodes[ch[s]];
             const int gc[2] = {cn.d.x, cn.d.y};
             for (int g = 0; g < 2; ++g) {
@@ -300,7 +338,7 @@ __global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, cons
                     lo[a][k] = l[a];
                     hi[a][k] = h[a];
                 }
-                ref[k++] = gc[g] >= 0 ? idx4[gc[g]] : gc[g];
+                ref[k++] = gc[g] >= 0 ? sub(gc[g]) : gc[g];
             }
         } else {
             float l[3], h[3];
@@ -309,7 +347,7 @@ __global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, cons
                 lo[a][k] = l[a];
                 hi[a][k] = h[a];
             }
-            ref[k++] = ch[s];
+            ref[k++] = (ch[s] >= 0 && n > 1) ? sub(ch[s]) : ch[s];
         }
     }
     for (; k < 4; ++k) {
@@ -333,7 +371,7 @@ __global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, cons
 
 struct Layout {
     size_t keys_a, keys_b, vals_a, vals_b, plo, phi, tri_rank, is_sph, sph_idx, slo, shi, leaf_ref, leaf_parent,
-        node_parent, flags, even, idx4, depth, cub, total;
+        node_parent, flags, even, idx4, depth, range, gate_pos, small, cub, total;
     size_t cub_bytes;
 };
 
@@ -365,6 +403,9 @@ Layout layout(int n) {
     L.even = take(sizeof(int) * n);
     L.idx4 = take(sizeof(int) * n);
     L.depth = take(2 * sizeof(int));  // depth, 4-wide node count
+    L.range = take(sizeof(int2) * n);
+    L.gate_pos = take(sizeof(int) * n);
+    L.small = take(sizeof(int) * n);
     size_t sort_bytes = 0, scan_bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (unsigned long long *)nullptr,
                                              (unsigned long long *)nullptr, (int *)nullptr, (int *)nullptr, n);
@@ -398,6 +439,8 @@ hipError_t build_lbvh_gpu(const LbvhInput &in, const LbvhOutput &out, void *scra
     auto *slo = (float4 *)(b + L.slo), *shi = (float4 *)(b + L.shi);
     auto *leaf_ref = (int *)(b + L.leaf_ref), *leaf_parent = (int *)(b + L.leaf_parent);
     auto *node_parent = (int *)(b + L.node_parent), *flags = (int *)(b + L.flags);
+    auto *range = (int2 *)(b + L.range);
+    auto *gate_pos = (int *)(b + L.gate_pos), *small = (int *)(b + L.small);
     void *cub = b + L.cub;
 
     hipLaunchKernelGGL(k_prims, dim3(blocks_for(n)), dim3(kThreads), 0, stream, in, out, n, plo, phi, keys_a, vals_a,
@@ -411,10 +454,10 @@ hipError_t build_lbvh_gpu(const LbvhInput &in, const LbvhOutput &out, void *scra
     e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, is_sph, sph_idx, n, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_leaves, dim3(blocks_for(n)), dim3(kThreads), 0, stream, in, out, n, vals_b, sph_idx,
-                       tri_rank, plo, phi, slo, shi, leaf_ref);
+                       tri_rank, plo, phi, slo, shi, leaf_ref, gate_pos);
     hipLaunchKernelGGL(k_karras, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n,
                        rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), keys_b, leaf_ref, slo, shi,
-                       out.nodes, leaf_parent, node_parent);
+                       out.nodes, leaf_parent, node_parent, range);
     e = hipMemsetAsync(flags, 0, sizeof(int) * n, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_bounds, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, slo, shi, leaf_parent,
@@ -424,17 +467,25 @@ hipError_t build_lbvh_gpu(const LbvhInput &in, const LbvhOutput &out, void *scra
     if (e != hipSuccess) return e;
     if (n > 1) {
         int *even = (int *)(b + L.even), *idx4 = (int *)(b + L.idx4);
-        hipLaunchKernelGGL(k_depth, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, node_parent, even, depth);
+        hipLaunchKernelGGL(k_small, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, range, gate_pos, small);
+        if (!out.nodes4) {  // 2-wide output: no collapsed leaves
+            e = hipMemsetAsync(small, 0, sizeof(int) * n, stream);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(k_depth, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, node_parent, small, even,
+                           depth);
         if (out.nodes4) {
             cub_bytes = L.cub_bytes;
             e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, even, idx4, n - 1, stream);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(k_collapse, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n,
-                               rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, even, idx4, out.nodes4, depth);
+                               rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, even, idx4, small, range,
+                               sph_idx, is_sph, out.nodes4, depth);
         }
     } else if (out.nodes4) {
         hipLaunchKernelGGL(k_collapse, dim3(1), dim3(kThreads), 0, stream, n,
-                           rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, nullptr, nullptr, out.nodes4, depth);
+                           rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, nullptr, nullptr, nullptr,
+                           nullptr, nullptr, nullptr, out.nodes4, depth);
     }
     return hipGetLastError();
 }
