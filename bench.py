@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: check the assembled frame against 1 rank")
     ap.add_argument("--mode", choices=["megakernel", "wavefront", "packet"], default="megakernel")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the distributed path (process group, async gather, reassembly) even at one rank")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU, "
                          "gather through host memory)")
@@ -98,10 +100,11 @@ def main():
     if world != args.gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     gloo = args.dist_backend == "gloo"
+    dist_on = world > 1 or args.force_dist
     ndev = torch.cuda.device_count()
     device = local_rank % ndev if gloo else local_rank
     torch.cuda.set_device(device)
-    if world > 1:
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if gloo:
             dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -117,17 +120,17 @@ def main():
     rx, ry = fr.plane.ResolutionX, fr.plane.ResolutionY
     R = 8
     band_count = world
-    local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if world > 1 else ry
+    local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if dist_on else ry
     # N > 1: two frame buffers, so the gather of frame k (RCCL, async) runs
     # while frame k+1 renders; rank 0 reassembles frame k once its gather is in
-    nbuf = 2 if world > 1 else 1
+    nbuf = 2 if dist_on else 1
     outs = [torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
     out = outs[0]
     nbytes = out.numel() * 4
     mode_flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET}.get(args.mode, 0)
-    params = rt.frame_params(fr, band_index=rank if world > 1 else 0, band_count=band_count, band_rows=R,
+    params = rt.frame_params(fr, band_index=rank if dist_on else 0, band_count=band_count, band_rows=R,
                              flags=mode_flags)
-    if world > 1:
+    if dist_on:
         gath = [torch.empty((world, local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)] \
             if rank == 0 else [None] * nbuf
         image = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
@@ -169,7 +172,7 @@ def main():
         b = frame_no[0] % nbuf
         finish_gather(b)  # buffer b is free again
         ctx.render_device(fr.camera, fr.plane, aparams, outs[b].data_ptr(), nbytes)
-        if world > 1:
+        if dist_on:
             begin_gather(b)
             finish_gather((b + nbuf - 1) % nbuf)  # the previous frame, gathered while this one rendered
         frame_no[0] += 1
@@ -188,7 +191,7 @@ def main():
         step()
     drain()
     ctx.finish()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -197,7 +200,7 @@ def main():
     drain()
     st = ctx.finish()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     rays = st.primary_rays + st.shadow_rays + st.reflection_rays
@@ -207,7 +210,7 @@ def main():
         ctx.render_device(fr.camera, fr.plane, aparams, out.data_ptr(), nbytes)
     kernel_ms = ctx.finish().kernel_ms
 
-    if world > 1 and args.verify:
+    if dist_on and args.verify:
         # the assembled frame must be bit-identical to a single-rank frame
         full = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda")
         if rank == 0:
@@ -217,7 +220,7 @@ def main():
             print(json.dumps({"verify_sharded_equals_single": same}), file=sys.stderr, flush=True)
             if not same:
                 raise SystemExit("sharded frame differs from the single-rank frame")
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed, float(rays), kernel_ms], dtype=torch.float64,
                          device="cpu" if gloo else "cuda")
         tmax = t.clone()
@@ -253,7 +256,7 @@ def main():
                 "depth": fr.max_bounces,
                 "triangles": fr.scene.triangle_count,
                 "parallelism": f"row-bands x{world}" + ((" + gloo gather (rehearsal)" if gloo else " + RCCL gather")
-                                                        if world > 1 else ""),
+                                                        if dist_on else ""),
                 "rays_per_frame": rays // args.steps,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
             },
@@ -274,7 +277,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(rt, fr, args.cpu_seconds)
         print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
