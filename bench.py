@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: check the assembled frame against 1 rank")
     ap.add_argument("--mode", choices=["megakernel", "wavefront", "packet"], default="megakernel")
+    ap.add_argument("--streams", type=int, default=2, help="N=1: HIP streams consecutive frames alternate on")
+    ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed path (process group, async gather, reassembly) even at one rank")
     ap.add_argument("--dist-backend", default="nccl",
@@ -113,7 +115,8 @@ def main():
 
     rt = _rt_pkg.load()
     fr = rt.make(args.config)
-    ctx = rt.Context()
+    ctx = rt.Context(lib_path=os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", args.lib, "librt_mi355.so")
+                     if args.lib else None)
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream.cuda_stream)
     ctx.set_scene(fr.scene)
@@ -123,7 +126,11 @@ def main():
     local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if dist_on else ry
     # N > 1: two frame buffers, so the gather of frame k (RCCL, async) runs
     # while frame k+1 renders; rank 0 reassembles frame k once its gather is in
-    nbuf = 2 if dist_on else 1
+    # N = 1: consecutive frames alternate between `--streams` HIP streams (own
+    # output buffers), so one frame's tail overlaps the next frame's start
+    nstreams = 1 if dist_on else max(1, args.streams)
+    nbuf = 2 if dist_on else nstreams
+    streams = [stream] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     outs = [torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
     out = outs[0]
     nbytes = out.numel() * 4
@@ -170,6 +177,8 @@ def main():
 
     def step():
         b = frame_no[0] % nbuf
+        if nstreams > 1:
+            ctx.set_stream(streams[b].cuda_stream)
         finish_gather(b)  # buffer b is free again
         ctx.render_device(fr.camera, fr.plane, aparams, outs[b].data_ptr(), nbytes)
         if dist_on:
@@ -199,6 +208,7 @@ def main():
         step()
     drain()
     st = ctx.finish()
+    ctx.set_stream(stream.cuda_stream)
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
@@ -258,6 +268,7 @@ def main():
                 "parallelism": f"row-bands x{world}" + ((" + gloo gather (rehearsal)" if gloo else " + RCCL gather")
                                                         if dist_on else ""),
                 "rays_per_frame": rays // args.steps,
+                "frames_in_flight": nstreams if not dist_on else 2,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
             },
             "roofline": {

@@ -149,9 +149,11 @@ typedef struct rt_render_params {
 #define RT_FLAG_OUT_RGBA8   8   /* Color32: round-half-even(clamp01(c) * 255), alpha 255; 4 B */
 #define RT_FLAG_OUT_RGBA16F 16  /* IEEE half RGBA (round to nearest even), alpha 1, unclamped; 8 B */
 /* rt_render_device only: enqueue the frame on the context's stream and return
- * without waiting (a frame loop that keeps the GPU fed).  The stats argument
- * is zeroed; rt_finish waits and returns the counters and device time of all
- * asynchronous frames since the previous rt_finish. */
+ * without waiting (a frame loop that keeps the GPU fed; switching the stream
+ * with rt_set_stream between frames lets consecutive frames overlap).  The
+ * stats argument is zeroed; rt_finish waits for the device and returns the
+ * counters and device time of all asynchronous frames since the previous
+ * rt_finish. */
 #define RT_FLAG_ASYNC       32
 
 /* Work counters and timings of the last render. */

@@ -29,9 +29,15 @@ namespace rtd {
 #define RT_STACK_LDS 24
 #endif
 constexpr int kStackSize = RT_STACK_LDS;  // LDS traversal stack entries per lane
-constexpr int kStackTotal = 128;          // + private (scratch) overflow: >= 3 * BVH4 depth, >= LBVH depth
+#ifndef RT_STACK_TOTAL
+#define RT_STACK_TOTAL 128
+#endif
+constexpr int kStackTotal = RT_STACK_TOTAL;          // + private (scratch) overflow: >= 3 * BVH4 depth, >= LBVH depth
 constexpr int kMaxTreeDepth = 31;         // builder guarantees BVH2 internal depth <= 31
-constexpr int kMaxBounces = 32;     // per-lane mirror fold stack
+#ifndef RT_MAX_BOUNCES
+#define RT_MAX_BOUNCES 32
+#endif
+constexpr int kMaxBounces = RT_MAX_BOUNCES;     // per-lane mirror fold stack
 constexpr int kWaveSize = 64;
 constexpr int kBlockThreads = 256;  // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;
@@ -162,6 +168,7 @@ struct FrameDev {
     int local_rows;          // rows of the compact output buffer
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
+    int tile_base, tile_stride;  // megakernel launch share: tiles tile_base + k * tile_stride
     void *out;               // local_rows x res_x pixels in out_format
     int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order

@@ -130,6 +130,9 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
 #define RT_MK_WAVES 1
 #endif
 constexpr int kMkWaves = RT_MK_WAVES;
+#ifndef RT_TILE_ORDER
+#define RT_TILE_ORDER 0
+#endif
 constexpr int kMkThreads = kMkWaves * kWaveSize;
 
 // Persistent megakernel: the grid holds exactly the resident wave slots and
@@ -184,8 +187,21 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x * kMkWaves + wave;
     if (!RT_MK_PERSIST) {
-        if (wid >= F.num_tiles) return;  // wave-uniform
-        render_tile<COUNT>(S, F, st, wstack, wid, lane, cnt);
+        // this launch's share of the tiles: tile_base, tile_base + tile_stride, ...
+        int tile = F.tile_base + wid * F.tile_stride;
+        if (tile >= F.num_tiles) return;  // wave-uniform
+#if RT_TILE_ORDER == 1
+        tile = F.num_tiles - 1 - tile;  // bottom rows first
+#elif RT_TILE_ORDER == 2
+        tile = (int)(((long long)tile * 1021) % F.num_tiles);  // spread (1021 prime)
+#elif RT_TILE_ORDER == 3
+        {  // tile rows from the bottom, each row left to right
+            const int row = tile / F.tiles_x;
+            tile = (F.num_tiles / F.tiles_x - 1 - row) * F.tiles_x + (tile - row * F.tiles_x);
+            if (tile < 0) tile += F.tiles_x;  // partial last row
+        }
+#endif
+        render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt);
     } else {
         const int nw = gridDim.x * kMkWaves;
         const int home = wid & (kTicketShards - 1);
@@ -366,7 +382,9 @@ bool mega_uses_tickets() { return RT_MK_PERSIST != 0; }
 
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
-    int blocks = (F.num_tiles + kMkWaves - 1) / kMkWaves;
+    const int my_tiles = F.tile_base < F.num_tiles ? (F.num_tiles - F.tile_base + F.tile_stride - 1) / F.tile_stride : 0;
+    if (my_tiles <= 0) return hipSuccess;
+    int blocks = (my_tiles + kMkWaves - 1) / kMkWaves;
     if (RT_MK_PERSIST) {
         // resident workgroups: occupancy per CU x CUs (queried once)
         static int resident = 0;
