@@ -124,12 +124,14 @@ def main():
     R = 8
     band_count = world
     local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if dist_on else ry
-    # N > 1: two frame buffers, so the gather of frame k (RCCL, async) runs
-    # while frame k+1 renders; rank 0 reassembles frame k once its gather is in
-    # N = 1: consecutive frames alternate between `--streams` HIP streams (own
-    # output buffers), so one frame's tail overlaps the next frame's start
-    nstreams = 1 if dist_on else max(1, args.streams)
-    nbuf = 2 if dist_on else nstreams
+    # Frames alternate between `--streams` HIP streams, each with its own output
+    # buffer: one frame's tail overlaps the next frame's start (two frames in
+    # flight).  N > 1: each buffer's shard is gathered to rank 0 over RCCL
+    # asynchronously (the NCCL stream waits for that buffer's stream) while the
+    # next frames render; rank 0 reassembles a frame when its buffer comes round
+    # again (or at the end).
+    nstreams = max(1, args.streams)
+    nbuf = nstreams
     streams = [stream] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     outs = [torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
     out = outs[0]
@@ -140,7 +142,8 @@ def main():
     if dist_on:
         gath = [torch.empty((world, local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)] \
             if rank == 0 else [None] * nbuf
-        image = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+        images = [torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)] \
+            if rank == 0 else [None] * nbuf
         if gloo:  # host staging buffers for the rehearsal backend
             outs_h = [torch.empty((local_rows, rx, 4), dtype=torch.float32) for _ in range(nbuf)]
             gath_h = [torch.empty((world, local_rows, rx, 4), dtype=torch.float32) for _ in range(nbuf)] \
@@ -167,7 +170,7 @@ def main():
         if rank == 0:
             if gloo:
                 gath[b].copy_(gath_h[b])
-            ctx.assemble_bands(gath[b].data_ptr(), rx, ry, world, R, image.data_ptr())
+            ctx.assemble_bands(gath[b].data_ptr(), rx, ry, world, R, images[b].data_ptr())
 
     # Frames are enqueued asynchronously (RT_FLAG_ASYNC): the host keeps the
     # stream fed and rt_finish returns the summed counters of the timed frames.
@@ -177,18 +180,21 @@ def main():
 
     def step():
         b = frame_no[0] % nbuf
-        if nstreams > 1:
+        with torch.cuda.stream(streams[b]):
             ctx.set_stream(streams[b].cuda_stream)
-        finish_gather(b)  # buffer b is free again
-        ctx.render_device(fr.camera, fr.plane, aparams, outs[b].data_ptr(), nbytes)
-        if dist_on:
-            begin_gather(b)
-            finish_gather((b + nbuf - 1) % nbuf)  # the previous frame, gathered while this one rendered
+            finish_gather(b)  # buffer b's previous frame: gathered and reassembled; the buffer is free
+            ctx.render_device(fr.camera, fr.plane, aparams, outs[b].data_ptr(), nbytes)
+            if dist_on:
+                begin_gather(b)
         frame_no[0] += 1
 
     def drain():
         for k in range(nbuf):
-            finish_gather((frame_no[0] + k) % nbuf)
+            b = (frame_no[0] + k) % nbuf
+            with torch.cuda.stream(streams[b]):
+                ctx.set_stream(streams[b].cuda_stream)
+                finish_gather(b)
+        ctx.set_stream(stream.cuda_stream)
 
     # counting launch (untimed): algorithmic work of this rank's frame
     cparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
@@ -226,7 +232,8 @@ def main():
         if rank == 0:
             ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=mode_flags), full.data_ptr(),
                               full.numel() * 4)
-            same = bool(torch.equal(full.view(torch.int32), image.view(torch.int32)))
+            last = images[(frame_no[0] - 1) % nbuf]
+            same = bool(torch.equal(full.view(torch.int32), last.view(torch.int32)))
             print(json.dumps({"verify_sharded_equals_single": same}), file=sys.stderr, flush=True)
             if not same:
                 raise SystemExit("sharded frame differs from the single-rank frame")
@@ -268,7 +275,7 @@ def main():
                 "parallelism": f"row-bands x{world}" + ((" + gloo gather (rehearsal)" if gloo else " + RCCL gather")
                                                         if dist_on else ""),
                 "rays_per_frame": rays // args.steps,
-                "frames_in_flight": nstreams if not dist_on else 2,
+                "frames_in_flight": nstreams,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
             },
             "roofline": {
