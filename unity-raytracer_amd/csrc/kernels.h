@@ -28,10 +28,6 @@ hipError_t launch_render_wavefront(const rtd::SceneDev &S, const rtd::FrameDev &
 hipError_t launch_intersect(const rtd::SceneDev &S, const float *rays, int n, int4 *out,
                             hipStream_t stream);
 
-// True when the megakernel is the persistent variant (tile tickets in
-// FrameDev.tickets must be zero at each launch).
-bool mega_uses_tickets();
-
 // Row-order reassembly of block-cyclic shards gathered back to back.
 hipError_t launch_assemble(const void *gathered, int res_x, int res_y, int band_count, int band_rows,
                            int local_rows, int pixel_bytes, void *image, hipStream_t stream);

@@ -86,9 +86,6 @@ struct rt_ctx {
     int4 *d_hits = nullptr;
     size_t rays_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    // helper streams of the split megakernel launch (fork/join events)
-    hipStream_t side[7] = {};
-    hipEvent_t ev_fork = nullptr, ev_join[7] = {};
     // RT_FLAG_ASYNC frames: pending count, accumulated counters and device time
     hipEvent_t ev_a0 = nullptr, ev_a1 = nullptr;
     int async_frames = 0;
@@ -376,41 +373,10 @@ int settle_async(rt_ctx *ctx) {
     return RT_OK;
 }
 
-// The megakernel launched as kMkParts interleaved shares of the tiles on
-// the context's stream and kMkParts - 1 helper streams (fork/join with events):
-// the launches are dispatched by separate hardware queues and overlap, which
-// keeps more waves resident than one launch does (measured +40 % on C3).
-#ifndef RT_MK_PARTS
-#define RT_MK_PARTS 1
-#endif
-constexpr int kMkParts = RT_MK_PARTS;
-
-hipError_t launch_mega_split(rt_ctx *ctx, rtd::FrameDev &F, bool count) {
-    if (kMkParts <= 1 || F.num_tiles < 2 * kMkParts) {
-        F.tile_base = 0;
-        F.tile_stride = 1;
-        return rtk::launch_render_mega(ctx->S, F, count, ctx->stream);
-    }
-    hipError_t e = hipEventRecord(ctx->ev_fork, ctx->stream);
-    for (int p = 1; p < kMkParts && e == hipSuccess; ++p) e = hipStreamWaitEvent(ctx->side[p - 1], ctx->ev_fork, 0);
-    for (int p = 0; p < kMkParts && e == hipSuccess; ++p) {
-        rtd::FrameDev Fp = F;
-        Fp.tile_base = p;
-        Fp.tile_stride = kMkParts;
-        e = rtk::launch_render_mega(ctx->S, Fp, count, p == 0 ? ctx->stream : ctx->side[p - 1]);
-    }
-    for (int p = 1; p < kMkParts && e == hipSuccess; ++p) {
-        e = hipEventRecord(ctx->ev_join[p - 1], ctx->side[p - 1]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, ctx->ev_join[p - 1], 0);
-    }
-    return e;
-}
-
 int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *d_out, rt_stats *stats,
               std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes) {
     F.out = d_out;
     F.counters = ctx->d_counters;
-    F.tickets = (unsigned *)(ctx->d_counters + rtd::kCounterSlots * rtd::kCounterWords);
     const bool count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
     const bool packet = (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
     const bool wavefront = !packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
@@ -430,19 +396,17 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
     if (!async || ctx->async_frames == 0) {
         // async frames share one set of counters until rt_finish / the next synchronous frame
-        HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes + rtd::kTicketBytes, ctx->stream));
+        HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes, ctx->stream));
         HIP_OR_FAIL(ctx, hipEventRecord(async ? ctx->ev_a0 : ctx->ev0, ctx->stream));
     } else {
         // a later async frame may be on another stream (rt_set_stream between
         // frames): it must not count before the counters were zeroed
         HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_a0, 0));
-        if (mega && rtk::mega_uses_tickets())
-            HIP_OR_FAIL(ctx, hipMemsetAsync(F.tickets, 0, rtd::kTicketBytes, ctx->stream));
     }
     if (packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));
     else if (mega)
-        HIP_OR_FAIL(ctx, launch_mega_split(ctx, F, count));
+        HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, count, ctx->stream));
     else if (wavefront && F.num_tiles > 0)
         HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, count, ctx->stream));
     if (async) {
@@ -686,21 +650,11 @@ int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev_a0) != hipSuccess || hipEventCreate(&c->ev_a1) != hipSuccess ||
         hipMalloc(&c->d_counters,
-                  rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long) + rtd::kTicketBytes) !=
+                  rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long)) !=
             hipSuccess) {
         rt_destroy(c);
         return fail(nullptr, RT_E_HIP, "stream/event/counter allocation failed");
     }
-    if (hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess) {
-        rt_destroy(c);
-        return fail(nullptr, RT_E_HIP, "event allocation failed");
-    }
-    for (int p = 0; p + 1 < kMkParts; ++p)
-        if (hipStreamCreateWithFlags(&c->side[p], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_join[p], hipEventDisableTiming) != hipSuccess) {
-            rt_destroy(c);
-            return fail(nullptr, RT_E_HIP, "helper stream allocation failed");
-        }
     c->stream = c->own_stream;
     *out_ctx = c;
     return RT_OK;
@@ -719,11 +673,6 @@ void rt_destroy(rt_ctx *ctx) {
     if (ctx->d_rays) (void)hipFree(ctx->d_rays);
     if (ctx->d_hits) (void)hipFree(ctx->d_hits);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
-    for (int p = 0; p < 7; ++p) {
-        if (ctx->side[p]) (void)hipStreamDestroy(ctx->side[p]);
-        if (ctx->ev_join[p]) (void)hipEventDestroy(ctx->ev_join[p]);
-    }
     if (ctx->ev_a0) (void)hipEventDestroy(ctx->ev_a0);
     if (ctx->ev_a1) (void)hipEventDestroy(ctx->ev_a1);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

@@ -47,7 +47,6 @@ constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;
 // serialise every wave's atomics (a single word saturates near 88 atomics/us).
 constexpr int kCounterSlots = 256;
 constexpr int kCounterWords = 8;
-constexpr int kTicketBytes = 256 * 64;  // tile tickets of the persistent megakernel (<= 256 shards x 64 B)
 
 constexpr int kLeafTri = 0;
 constexpr int kLeafSphere = 1;
@@ -168,11 +167,9 @@ struct FrameDev {
     int local_rows;          // rows of the compact output buffer
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
-    int tile_base, tile_stride;  // megakernel launch share: tiles tile_base + k * tile_stride
     void *out;               // local_rows x res_x pixels in out_format
     int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
-    unsigned *tickets;             // persistent megakernel tile tickets (shards x 64 B), zeroed per frame
 };
 
 }  // namespace rtd

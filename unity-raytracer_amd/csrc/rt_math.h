@@ -68,10 +68,6 @@ RT_HD bool ref_slab(f3 o, f3 inv, f3 lo, f3 hi) {
     return tmin <= tmax;
 }
 
-#ifndef RT_MT_EARLY
-#define RT_MT_EARLY 0
-#endif
-
 // RMath.RayTriangleIntersection (RMath.cs:29-73), with edge1 = v1 - v0 and
 // edge2 = v2 - v0 precomputed on the host (the same two float subtractions).
 RT_HD bool ref_triangle(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float &t_out) {
@@ -80,20 +76,6 @@ RT_HD bool ref_triangle(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float &t_out) {
     if (a > -kEpsilon && a < kEpsilon) return false;
     f3 s = o - v0;
     const float sh = dot(s, h);
-#if RT_MT_EARLY
-    // The reference rejects on u = fl(fl(1/a) * sh) < 0 or > 1.  Decide that
-    // without the division when it is certain: fl(1/a) and the product each
-    // round by <= 2^-24 relative, so |sh| > |a|(1 + 2^-20) with the sign of a
-    // gives u > 1, and opposite signs with |sh| > |a| * 2^-100 (far from
-    // underflow, where u could round to -0) give u < 0.  Anything closer takes
-    // the exact path below, so every decision equals the reference's.
-    {
-        const float aa = fabsf(a), as = fabsf(sh);
-        const bool same = (a > 0.0f) == (sh > 0.0f);
-        if (!same && sh != 0.0f && as > aa * 0x1p-100f) return false;
-        if (same && as > aa * (1.0f + 0x1p-20f)) return false;
-    }
-#endif
     float f = 1.0f / a;
     float u = f * sh;
     if (u < 0.0f || u > 1.0f) return false;

@@ -84,11 +84,7 @@ __device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &
         // pow(float, float) = (float)System.Math.Pow((double)x, (double)y); a
         // material whose specular term is always a signed zero skips it
         // (ks.w, rt_abi.cpp to_dev): (ks * 0) * E has the same bits.
-#if RT_EXP_FLOAT_POW  // timing experiment only (not the reference's rounding): cost of the double pow
-        const float pw = powf(cnh, m.kd_phong.w);
-#else
         const float pw = m.ks.w != 0.0f ? 0.0f : spec_pow(cnh, m.kd_phong.w);
-#endif
         spec = (mk(m.ks.x, m.ks.y, m.ks.z) * pw) * e;
     }
     return diffuse + spec;

@@ -87,7 +87,6 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
             rtt::setup_ray(rs, sr.o, sr.dir);
             float dt;
             int dr;
-#if !RT_EXP_NO_SHADOW  // timing experiment only (wrong images): cost of the shadow queries
             if (!COUNT && RT_MK_PACKET_SHADOW && depth < RT_MK_PACKET_DEPTHS && S.bvh4) {
                 rtp::PacketLane Q;
                 rtp::packet_trace<true, COUNT>(S, rs, true, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
@@ -95,11 +94,6 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
             } else if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) {
                 continue;
             }
-#endif
-#if RT_RELOAD
-            // keep material/light out of registers across the traversal
-            asm volatile("" ::: "memory");
-#endif
             col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
         }
         const DevMaterial m = S.mats[sf.mat];
@@ -130,23 +124,8 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
 #define RT_MK_WAVES 1
 #endif
 constexpr int kMkWaves = RT_MK_WAVES;
-#ifndef RT_TILE_ORDER
-#define RT_TILE_ORDER 0
-#endif
 constexpr int kMkThreads = kMkWaves * kWaveSize;
 
-// Persistent megakernel: the grid holds exactly the resident wave slots and
-// every wave loops over tiles: first its own id, then tickets from 8
-// sharded counters (shard c hands out tiles nw + c + kTicketShards*k; an exhausted shard
-// sends the wave to the next one), so no slot idles while tiles remain.
-#ifndef RT_MK_PERSIST
-#define RT_MK_PERSIST 0
-#endif
-#ifndef RT_TICKET_SHARDS
-#define RT_TICKET_SHARDS 64
-#endif
-constexpr int kTicketShards = RT_TICKET_SHARDS;
-constexpr int kTicketStride = 16;  // one 64-byte line per shard
 
 // One tile (a wave) of the megakernel: trace every sample, sum a pixel's
 // samples in row-major sample order ((s0 + s1) + s2) + ..., store.
@@ -185,56 +164,9 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
     int *const wstack = wstack_mem + (kPackets ? wave * rtp::kWaveStack : 0);
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
-    const int wid = blockIdx.x * kMkWaves + wave;
-    if (!RT_MK_PERSIST) {
-        // this launch's share of the tiles: tile_base, tile_base + tile_stride, ...
-        int tile = F.tile_base + wid * F.tile_stride;
-        if (tile >= F.num_tiles) return;  // wave-uniform
-#if RT_TILE_ORDER == 1
-        tile = F.num_tiles - 1 - tile;  // bottom rows first
-#elif RT_TILE_ORDER == 2
-        tile = (int)(((long long)tile * 1021) % F.num_tiles);  // spread (1021 prime)
-#elif RT_TILE_ORDER == 3
-        {  // tile rows from the bottom, each row left to right
-            const int row = tile / F.tiles_x;
-            tile = (F.num_tiles / F.tiles_x - 1 - row) * F.tiles_x + (tile - row * F.tiles_x);
-            if (tile < 0) tile += F.tiles_x;  // partial last row
-        }
-#endif
-        render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt);
-    } else {
-        const int nw = gridDim.x * kMkWaves;
-        const int home = wid & (kTicketShards - 1);
-        unsigned *const home_ctr = F.tickets + home * kTicketStride;
-        // the next ticket is requested before the current tile is traced, so
-        // its atomic round trip overlaps the tile's first node fetches
-        unsigned q = 0;
-        if (lane == 0) q = atomicAdd(home_ctr, 1u);
-        int tile = wid;
-        while (tile < F.num_tiles) {  // wave-uniform
-            render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt);
-            int next = 0x7fffffff;
-            if (lane == 0) {
-                const long long cand = (long long)nw + home + (long long)kTicketShards * q;
-                if (cand < F.num_tiles) {
-                    next = (int)cand;
-                    q = atomicAdd(home_ctr, 1u);
-                } else {
-                    // home shard exhausted: take from the others (end of frame only)
-                    for (int k = 1; k < kTicketShards; ++k) {
-                        const int c = (home + k) & (kTicketShards - 1);
-                        const unsigned r = atomicAdd(F.tickets + c * kTicketStride, 1u);
-                        const long long cc = (long long)nw + c + (long long)kTicketShards * r;
-                        if (cc < F.num_tiles) {
-                            next = (int)cc;
-                            break;
-                        }
-                    }
-                }
-            }
-            tile = __builtin_amdgcn_readfirstlane(next);
-        }
-    }
+    const int tile = blockIdx.x * kMkWaves + wave;
+    if (tile >= F.num_tiles) return;  // wave-uniform
+    render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt);
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
 
@@ -378,28 +310,9 @@ __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int ba
 
 namespace rtk {
 
-bool mega_uses_tickets() { return RT_MK_PERSIST != 0; }
-
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
-    const int my_tiles = F.tile_base < F.num_tiles ? (F.num_tiles - F.tile_base + F.tile_stride - 1) / F.tile_stride : 0;
-    if (my_tiles <= 0) return hipSuccess;
-    int blocks = (my_tiles + kMkWaves - 1) / kMkWaves;
-    if (RT_MK_PERSIST) {
-        // resident workgroups: occupancy per CU x CUs (queried once)
-        static int resident = 0;
-        if (resident == 0) {
-            int dev = 0, cus = 0, per_cu = 0;
-            hipError_t e = hipGetDevice(&dev);
-            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            if (e == hipSuccess)
-                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(
-                                                                    &render_kernel<false>), kMkThreads, 0);
-            if (e != hipSuccess) return e;
-            resident = std::max(1, cus * per_cu);
-        }
-        blocks = std::min(blocks, resident);
-    }
+    const int blocks = (F.num_tiles + kMkWaves - 1) / kMkWaves;
     if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else

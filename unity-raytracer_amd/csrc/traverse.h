@@ -24,38 +24,15 @@ struct Counts {
     unsigned primary, shadow, reflection, box, tri, sph, shading;
 };
 
-// RT_LEAN_RAY: keep only o, d and the node-test reciprocal in registers; the
-// exact 1/d (scene and mesh gates, rare) and o * ninv (once per node) are
-// recomputed where used — identical values, six fewer live registers across
-// every traversal.
-#ifndef RT_LEAN_RAY
-#define RT_LEAN_RAY 0
-#endif
-
 __device__ __forceinline__ float nudge(float v) { return fabsf(v) > 1e-20f ? v : copysignf(1e-20f, v); }
 
 struct RayCtx {
-    f3 o, d;  // exact ray (reference semantics)
-    f3 ninv;  // node-test inverse (zero components nudged, approximate rcp)
-#if !RT_LEAN_RAY
-    f3 inv_v, noi_v;
-#endif
-    // rcp(dir) = 1.0f / dir, exact — the reference's AABB gates
-    __device__ __forceinline__ f3 inv() const {
-#if RT_LEAN_RAY
-        return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-#else
-        return inv_v;
-#endif
-    }
-    // o * ninv
-    __device__ __forceinline__ f3 noi() const {
-#if RT_LEAN_RAY
-        return mk(o.x * ninv.x, o.y * ninv.y, o.z * ninv.z);
-#else
-        return noi_v;
-#endif
-    }
+    f3 o, d;     // exact ray (reference semantics)
+    f3 ninv;     // node-test inverse (zero components nudged, approximate rcp)
+    f3 inv_v;    // rcp(dir) = 1.0f / dir, exact — the reference's AABB gates
+    f3 noi_v;    // o * ninv
+    __device__ __forceinline__ f3 inv() const { return inv_v; }
+    __device__ __forceinline__ f3 noi() const { return noi_v; }
 };
 
 __device__ __forceinline__ void setup_ray(RayCtx &r, f3 o, f3 d) {
@@ -63,10 +40,8 @@ __device__ __forceinline__ void setup_ray(RayCtx &r, f3 o, f3 d) {
     r.d = d;
     r.ninv = mk(__builtin_amdgcn_rcpf(nudge(d.x)), __builtin_amdgcn_rcpf(nudge(d.y)),
                 __builtin_amdgcn_rcpf(nudge(d.z)));
-#if !RT_LEAN_RAY
     r.inv_v = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     r.noi_v = mk(o.x * r.ninv.x, o.y * r.ninv.y, o.z * r.ninv.z);
-#endif
 }
 
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
@@ -297,41 +272,20 @@ __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const 
     return false;
 }
 
-#ifndef RT_PK_FMA
-#define RT_PK_FMA 0
-#endif
-typedef float f2v __attribute__((ext_vector_type(2)));
 
 // Conservative slab test of one child of a 4-wide node: its entry distance,
 // or +inf when culled.
 __device__ __forceinline__ float child_key(float lx, float hx, float ly, float hy, float lz, float hz,
                                            const RayCtx &r, float tcull) {
     const f3 noi = r.noi();
-#if RT_PK_FMA
-    // packed FMA: both planes of an axis in one v_pk_fma_f32
-    const f2v px = __builtin_elementwise_fma((f2v){lx, hx}, (f2v){r.ninv.x, r.ninv.x}, (f2v){-noi.x, -noi.x});
-    const f2v py = __builtin_elementwise_fma((f2v){ly, hy}, (f2v){r.ninv.y, r.ninv.y}, (f2v){-noi.y, -noi.y});
-    const f2v pz = __builtin_elementwise_fma((f2v){lz, hz}, (f2v){r.ninv.z, r.ninv.z}, (f2v){-noi.z, -noi.z});
-    const float ax = px.x, bx = px.y, ay = py.x, by = py.y, az = pz.x, bz = pz.y;
-#else
     const float ax = fmaf(lx, r.ninv.x, -noi.x), bx = fmaf(hx, r.ninv.x, -noi.x);
     const float ay = fmaf(ly, r.ninv.y, -noi.y), by = fmaf(hy, r.ninv.y, -noi.y);
     const float az = fmaf(lz, r.ninv.z, -noi.z), bz = fmaf(hz, r.ninv.z, -noi.z);
-#endif
     const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
     const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tcull));
     return tn <= tf ? tn : INFINITY;
 }
 
-#ifndef RT_ANY_NOSORT
-#define RT_ANY_NOSORT 0
-#endif
-#ifndef RT_RELOAD
-#define RT_RELOAD 0
-#endif
-#ifndef RT_NEAR_ONLY
-#define RT_NEAR_ONLY 0
-#endif
 
 #define RT_CSWAP(i, j)                          \
     do {                                        \
@@ -362,28 +316,11 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         float k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, t.tcull);
         if (COUNT) cnt.box += 4;
         int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-        if (RT_NEAR_ONLY) {
-            // nearest child first, the others in slot order (3 compare-swaps)
-            RT_CSWAP(0, 1);
-            RT_CSWAP(0, 2);
-            RT_CSWAP(0, 3);
-            // hit children must precede misses for the push count below
-            RT_CSWAP(2, 3);
-            RT_CSWAP(1, 2);
-            RT_CSWAP(2, 3);
-        } else if (!ANY || !RT_ANY_NOSORT) {  // any-hit queries need no near-first order
-            RT_CSWAP(0, 1);
-            RT_CSWAP(2, 3);
-            RT_CSWAP(0, 2);
-            RT_CSWAP(1, 3);
-            RT_CSWAP(1, 2);
-        } else {
-            // compact the hit children to the front (order irrelevant)
-            RT_CSWAP(0, 1);
-            RT_CSWAP(2, 3);
-            RT_CSWAP(0, 2);
-            RT_CSWAP(1, 3);
-        }
+        RT_CSWAP(0, 1);  // sort the four keys (5 compare-swaps)
+        RT_CSWAP(2, 3);
+        RT_CSWAP(0, 2);
+        RT_CSWAP(1, 3);
+        RT_CSWAP(1, 2);
         if (k0 != INFINITY) {
             // push the other hit children far-first: bottom..top = c_{h-1} .. c1
             const int h = 1 + (k1 != INFINITY) + (k2 != INFINITY) + (k3 != INFINITY);
