@@ -123,7 +123,7 @@ namespace RayTracer.Native
         public const int OK = 0;
         public const int BuildSahHost = 0, BuildLbvhGpu = 1, BuildLbvhGpuBvh2 = 2;
         public const int FlagCountTests = 1, FlagWavefront = 2, FlagPacket = 4, FlagOutRgba8 = 8, FlagOutRgba16F = 16,
-                         FlagAsync = 32;
+                         FlagAsync = 32, FlagRowOrder = 64;
 
         [DllImport(Lib)] public static extern int rt_abi_version();
         [DllImport(Lib)] public static extern int rt_create(out IntPtr ctx, int numGpus);

@@ -155,6 +155,12 @@ typedef struct rt_render_params {
  * counters and device time of all asynchronous frames since the previous
  * rt_finish. */
 #define RT_FLAG_ASYNC       32
+/* Megakernel frames normally dispatch their tiles longest-first, ordered by
+ * the per-tile cost an earlier frame of the same layout and scene measured on
+ * the same stream (the frame's tail is its slowest tiles; re-measured every
+ * few frames).  This flag keeps row-major order.  Results never depend on the
+ * order. */
+#define RT_FLAG_ROW_ORDER   64
 
 /* Work counters and timings of the last render. */
 typedef struct rt_stats {

@@ -244,3 +244,25 @@ def test_async_frames(gpu_ctx, rt):
     assert tot.primary_rays == sr.primary_rays
     with pytest.raises(rt.RtError):
         gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC))
+
+
+def test_longest_first_order_is_invisible(gpu_ctx, rt):
+    """Synchronous frames after the first dispatch their tiles longest-first
+    (previous frame's costs); the frames stay bit-identical to row-major ones,
+    also when the layout or the scene changes in between."""
+    fr = rt.make("C3").with_resolution(320, 180)
+    gpu_ctx.set_scene(fr.scene)
+    row, _ = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER))
+    for _ in range(6):  # crosses a re-sort period
+        img, _ = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+        assert np.array_equal(img.view(np.uint32), row.view(np.uint32))
+    small = fr.with_resolution(64, 48)
+    a, _ = gpu_ctx.render(small.camera, small.plane, rt.frame_params(small))
+    b, _ = gpu_ctx.render(small.camera, small.plane, rt.frame_params(small, flags=rt.abi.RT_FLAG_ROW_ORDER))
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    fr2 = rt.make("C2").with_resolution(320, 180)
+    gpu_ctx.set_scene(fr2.scene)
+    for _ in range(3):
+        c, _ = gpu_ctx.render(fr2.camera, fr2.plane, rt.frame_params(fr2))
+    d, _ = gpu_ctx.render(fr2.camera, fr2.plane, rt.frame_params(fr2, flags=rt.abi.RT_FLAG_ROW_ORDER))
+    assert np.array_equal(c.view(np.uint32), d.view(np.uint32))

@@ -46,7 +46,8 @@ def main():
         out = torch.empty((fr.plane.ResolutionY, fr.plane.ResolutionX, 4), dtype=torch.float32, device="cuda")
         ref = None
         for mode in a.modes.split(","):
-            flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET}.get(mode, 0)
+            flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET,
+                     "rowmajor": rt.abi.RT_FLAG_ROW_ORDER}.get(mode, 0)
             p = rt.frame_params(fr, flags=flags)
             cst = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=flags | 1), out.data_ptr(),
                                     out.numel() * 4)

@@ -53,6 +53,26 @@ struct LbvhBufs {
     }
 };
 
+// Longest-first dispatch state of one stream: the last measured per-tile cost
+// keys, the order sorted from them, for one frame layout and scene version.
+struct LptSlot {
+    hipStream_t stream = nullptr;
+    bool used = false;
+    GrowBuf cost, cost_sorted, iota, order, scratch;
+    long long key = -1;
+    unsigned long long scene = ~0ull;
+    bool valid = false;
+    long long frames = 0;
+    void release() {
+        for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch}) {
+            if (b->p) (void)hipFree(b->p);
+            b->p = nullptr;
+            b->cap = 0;
+        }
+    }
+};
+constexpr int kLptSlots = 4;
+
 // State kept by rt_set_scene_source for rt_update_mesh_transforms.
 struct SourceState {
     bool active = false;
@@ -103,6 +123,11 @@ struct rt_ctx {
     int last_bvh_depth = 0;
     rt_scene_info info{};
     LbvhBufs lb;
+    // longest-first tile order of megakernel frames (a previous frame's
+    // per-tile cost), one state per stream the frames run on, so frames in
+    // flight on different streams never read an order being rewritten
+    LptSlot lpt[kLptSlots];
+    unsigned long long scene_version = 0;
     SourceState src;
 };
 
@@ -332,6 +357,30 @@ int prepare_wavefront(rt_ctx *ctx, const rtd::FrameDev &F, int &chunk_tiles, rtw
     return RT_OK;
 }
 
+// Grow-only device buffer (per-frame rebuilds reuse their memory).
+hipError_t ensure(rt_ctx *ctx, GrowBuf &b, size_t bytes) {
+    (void)ctx;
+    if (bytes <= b.cap) return hipSuccess;
+    if (b.p) {
+        hipError_t e = hipFree(b.p);
+        if (e != hipSuccess) return e;
+    }
+    b.p = nullptr;
+    b.cap = 0;
+    hipError_t e = hipMalloc(&b.p, bytes < 256 ? 256 : bytes);
+    if (e == hipSuccess) b.cap = bytes < 256 ? 256 : bytes;
+    return e;
+}
+
+template <typename T>
+hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
+    hipError_t e = ensure(ctx, b, count * sizeof(T));
+    if (e != hipSuccess || count == 0) return e;
+    return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
+}
+
+constexpr int kLptPeriod = 4;  // frames between longest-first re-sorts
+
 // Sums the sharded ray/test counters on the host (the stream must be idle).
 int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
     const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
@@ -403,6 +452,50 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         // frames): it must not count before the counters were zeroed
         HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_a0, 0));
     }
+    // megakernel frames dispatch a previous frame's most expensive tiles
+    // first (a frame's tail is its slowest tiles); the order is kept per stream
+    LptSlot *ls = nullptr;
+    bool lpt_sort = false;
+    F.tile_order = nullptr;
+    F.tile_cost = nullptr;
+    if (mega && (prm->flags & RT_FLAG_ROW_ORDER) == 0 && F.num_tiles > 0) {
+        for (LptSlot &l : ctx->lpt)
+            if (l.used && l.stream == ctx->stream) ls = &l;
+        if (!ls)
+            for (LptSlot &l : ctx->lpt)
+                if (!l.used && !ls) {
+                    ls = &l;
+                    ls->used = true;
+                    ls->stream = ctx->stream;
+                }
+    }
+    if (ls) {  // (more than kLptSlots streams: the extra ones keep row-major order)
+        const long long key = ((long long)F.num_tiles << 32) ^ ((long long)F.tiles_x << 20) ^
+                              ((long long)F.spp << 12) ^ ((long long)F.band_count << 6) ^ F.band_index;
+        if (key != ls->key) {
+            const size_t n = (size_t)F.num_tiles;
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->cost, n * 4));
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->cost_sorted, n * 4));
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->order, n * 4));
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->scratch, rtk::tile_sort_scratch_bytes(F.num_tiles)));
+            std::vector<int> iota(n);
+            for (size_t i = 0; i < n; ++i) iota[i] = (int)i;
+            HIP_OR_FAIL(ctx, put(ctx, ls->iota, iota.data(), n));
+            ls->key = key;
+            ls->valid = false;
+        }
+        if (ls->scene != ctx->scene_version) {
+            ls->scene = ctx->scene_version;
+            ls->valid = false;
+        }
+        if (!ls->valid) ls->frames = 0;
+        F.tile_order = ls->valid ? (const int *)ls->order.p : nullptr;
+        // costs are measured and re-sorted every kLptPeriod frames (the sort
+        // costs more than a small frame's tail)
+        lpt_sort = !ls->valid || ls->frames % kLptPeriod == 0;
+        F.tile_cost = lpt_sort ? (unsigned *)ls->cost.p : nullptr;
+        ++ls->frames;
+    }
     if (packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));
     else if (mega)
@@ -410,6 +503,12 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     else if (wavefront && F.num_tiles > 0)
         HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, count, ctx->stream));
     if (async) {
+        if (lpt_sort) {
+            HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
+                                                     (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
+                                                     ls->scratch.p, ls->scratch.cap, ctx->stream));
+            ls->valid = true;
+        }
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_a1, ctx->stream));
         if (ctx->async_frames++ == 0 && ctx->async_t0_set == false) {
             ctx->async_t0 = t_start;
@@ -419,6 +518,12 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         return RT_OK;
     }
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    if (lpt_sort) {  // after the timed region: the order of the next frames
+        HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
+                                                 (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
+                                                 ls->scratch.p, ls->scratch.cap, ctx->stream));
+        ls->valid = true;
+    }
     if (host_out && out_bytes)
         HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
@@ -434,28 +539,6 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     return RT_OK;
 }
 
-
-// Grow-only device buffer (per-frame rebuilds reuse their memory).
-hipError_t ensure(rt_ctx *ctx, GrowBuf &b, size_t bytes) {
-    (void)ctx;
-    if (bytes <= b.cap) return hipSuccess;
-    if (b.p) {
-        hipError_t e = hipFree(b.p);
-        if (e != hipSuccess) return e;
-    }
-    b.p = nullptr;
-    b.cap = 0;
-    hipError_t e = hipMalloc(&b.p, bytes < 256 ? 256 : bytes);
-    if (e == hipSuccess) b.cap = bytes < 256 ? 256 : bytes;
-    return e;
-}
-
-template <typename T>
-hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
-    hipError_t e = ensure(ctx, b, count * sizeof(T));
-    if (e != hipSuccess || count == 0) return e;
-    return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
-}
 
 // Scene.CalculateAABB (Scene.cs:17-41) with Unity min/max semantics:
 // mesh AABBs, then loose triangle vertices, then sphere boxes.
@@ -667,6 +750,7 @@ void rt_destroy(rt_ctx *ctx) {
     free_scene(ctx);
     free_wavefront(ctx);
     ctx->lb.release();
+    for (LptSlot &l : ctx->lpt) l.release();
     if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
@@ -732,6 +816,7 @@ int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geo
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     free_scene(ctx);
     ctx->info = rt_scene_info{};
+    ++ctx->scene_version;
 
     const int MT = (int)mesh_ranks, NS = sc->sphere_count, NL = sc->triangle_count;
     const int P = MT + NS + NL;
@@ -1020,6 +1105,7 @@ int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t 
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     LbvhBufs &B = ctx->lb;
+    ++ctx->scene_version;
     HIP_OR_FAIL(ctx, put(ctx, B.src_matrices, local_to_world, (size_t)mesh_count * 16));
     std::vector<rtd::MeshGate> aabbs;
     float xform_ms = 0.0f;

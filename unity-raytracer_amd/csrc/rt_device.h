@@ -168,6 +168,8 @@ struct FrameDev {
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
     void *out;               // local_rows x res_x pixels in out_format
+    const int *tile_order;   // megakernel dispatch order (null: row-major)
+    unsigned *tile_cost;     // per-tile cost of this frame (shader clock), null: not recorded
     int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
 };

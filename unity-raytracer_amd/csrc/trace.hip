@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include "kernels.h"
 #include "packet.h"
@@ -164,9 +165,18 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
     int *const wstack = wstack_mem + (kPackets ? wave * rtp::kWaveStack : 0);
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
-    const int tile = blockIdx.x * kMkWaves + wave;
-    if (tile >= F.num_tiles) return;  // wave-uniform
+    const int wid = blockIdx.x * kMkWaves + wave;
+    if (wid >= F.num_tiles) return;  // wave-uniform
+    // dispatch order: the previous frame's most expensive tiles first (F.tile_order)
+    const int tile = F.tile_order ? F.tile_order[wid] : wid;
+    const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt);
+    if (F.tile_cost && lane == 0) {
+        // log-scale cost key (4 mantissa bits, < 512): one cheap sort pass set
+        const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
+        const unsigned e = c ? 31u - __clz(c) : 0u;
+        F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
+    }
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
 
@@ -318,6 +328,22 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
     else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     return hipGetLastError();
+}
+
+// Longest-first dispatch for the next frame: tiles sorted by the cost key this
+// frame measured (descending, 9-bit log-scale keys).
+size_t tile_sort_scratch_bytes(int n) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, bytes, (const unsigned *)nullptr, (unsigned *)nullptr,
+                                                        (const int *)nullptr, (int *)nullptr, n, 0, 9);
+    return bytes;
+}
+
+hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const int *iota, int *order, int n,
+                              void *scratch, size_t scratch_bytes, hipStream_t stream) {
+    size_t bytes = scratch_bytes;
+    return hipcub::DeviceRadixSort::SortPairsDescending(scratch, bytes, cost, cost_sorted, iota, order, n, 0, 9,
+                                                        stream);
 }
 
 #ifndef RT_PACKET_LEVELS
