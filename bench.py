@@ -87,7 +87,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: check the assembled frame against 1 rank")
     ap.add_argument("--mode", choices=["megakernel", "wavefront", "packet"], default="megakernel")
-    ap.add_argument("--streams", type=int, default=2, help="N=1: HIP streams consecutive frames alternate on")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams consecutive frames alternate on (frames in flight; 1 = one frame at a time)")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed path (process group, async gather, reassembly) even at one rank")
@@ -124,14 +125,14 @@ def main():
     R = 8
     band_count = world
     local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if dist_on else ry
-    # Frames alternate between `--streams` HIP streams, each with its own output
-    # buffer: one frame's tail overlaps the next frame's start (two frames in
-    # flight).  N > 1: each buffer's shard is gathered to rank 0 over RCCL
-    # asynchronously (the NCCL stream waits for that buffer's stream) while the
-    # next frames render; rank 0 reassembles a frame when its buffer comes round
-    # again (or at the end).
+    # Frames rotate over nbuf output buffers and `--streams` HIP streams (more
+    # than one stream = frames in flight, off by default).  N > 1: each
+    # buffer's shard is gathered to rank 0 over RCCL asynchronously (the NCCL
+    # stream waits for the buffer's render stream) while the next frame
+    # renders; rank 0 reassembles a frame when its buffer comes round again
+    # (or at the end).
     nstreams = max(1, args.streams)
-    nbuf = nstreams
+    nbuf = max(nstreams, 2 if dist_on else 1)
     streams = [stream] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     outs = [torch.empty((local_rows, rx, 4), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
     out = outs[0]
@@ -180,8 +181,9 @@ def main():
 
     def step():
         b = frame_no[0] % nbuf
-        with torch.cuda.stream(streams[b]):
-            ctx.set_stream(streams[b].cuda_stream)
+        sb = streams[b % nstreams]
+        with torch.cuda.stream(sb):
+            ctx.set_stream(sb.cuda_stream)
             finish_gather(b)  # buffer b's previous frame: gathered and reassembled; the buffer is free
             ctx.render_device(fr.camera, fr.plane, aparams, outs[b].data_ptr(), nbytes)
             if dist_on:
@@ -191,8 +193,9 @@ def main():
     def drain():
         for k in range(nbuf):
             b = (frame_no[0] + k) % nbuf
-            with torch.cuda.stream(streams[b]):
-                ctx.set_stream(streams[b].cuda_stream)
+            sb = streams[b % nstreams]
+            with torch.cuda.stream(sb):
+                ctx.set_stream(sb.cuda_stream)
                 finish_gather(b)
         ctx.set_stream(stream.cuda_stream)
 
