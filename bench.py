@@ -266,6 +266,7 @@ def main():
 
     if rank == 0:
         avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's own trace kernel, HIP events
+        traffic = load_traffic(args.config)
         achieved = bytes_per_launch / avg_kernel_s / 1e9
         line = {
             "metric": METRIC,
@@ -299,11 +300,15 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(args.config),
+                "traffic": traffic,
                 "kernel": {"megakernel": "render_kernel<false>", "packet": "render_packet_kernel<false,1>"}.get(
                     args.mode, "wavefront passes (sum)"),
                 "bytes_per_launch": bytes_per_launch,
                 "avg_kernel_ms": avg_kernel_s * 1e3,
+                # rocprof-measured HBM bytes (PMC, profiles/pmc_<config>.json) per
+                # launch over the same launch time: the bandwidth actually drawn
+                "traffic_gbs": (traffic / avg_kernel_s / 1e9) if traffic else None,
+                "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
             },
         }
         if world == 1 and not args.no_cpu_baseline:
