@@ -183,13 +183,14 @@ def main():
         if rank == 0:
             if gloo:
                 gath[b].copy_(gath_h[b])
-            ctx.assemble_bands(gath[b].data_ptr(), rx, ry, world, R, images[b].data_ptr())
+            ctx.assemble_bands(gath[b].data_ptr(), rx, ry, world, R, images[b].data_ptr(), sync=False)
 
     # Frames are enqueued asynchronously (RT_FLAG_ASYNC): the host keeps the
     # stream fed and rt_finish returns the summed counters of the timed frames.
     aparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
                               flags=mode_flags | rt.abi.RT_FLAG_ASYNC)
     frame_no = [0]
+    cam_s, plane_s = rt.raytracing.camera_struct(fr.camera), rt.raytracing.plane_struct(fr.plane)
 
     def step():
         b = frame_no[0] % nbuf
@@ -197,7 +198,7 @@ def main():
         with torch.cuda.stream(sb):
             ctx.set_stream(sb.cuda_stream)
             finish_gather(b)  # buffer b's previous frame: gathered and reassembled; the buffer is free
-            ctx.render_device(fr.camera, fr.plane, aparams, outs[b].data_ptr(), nbytes)
+            ctx.render_device(cam_s, plane_s, aparams, outs[b].data_ptr(), nbytes)
             if dist_on:
                 begin_gather(b)
         frame_no[0] += 1

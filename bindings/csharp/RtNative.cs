@@ -147,6 +147,7 @@ namespace RayTracer.Native
                                                  out RtStats stats);
         [DllImport(Lib)] public static extern int rt_pixel_bytes(int flags);
         [DllImport(Lib)] public static extern int rt_finish(IntPtr ctx, out RtStats stats);
+        [DllImport(Lib)] public static extern int rt_synchronize(IntPtr ctx);
         [DllImport(Lib)] public static extern int rt_render_device(IntPtr ctx, ref CameraData cam,
                                                                   ref RtImagePlane plane, ref RtRenderParams p,
                                                                   IntPtr devicePixels, UIntPtr outBytes,

@@ -303,10 +303,15 @@ int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x
                       int32_t resolution_y, int32_t band_count, int32_t band_rows,
                       float *d_image);
 
-/* rt_assemble_bands for any output format: pixel_bytes = rt_pixel_bytes(flags). */
+/* rt_assemble_bands for any output format: pixel_bytes = rt_pixel_bytes(flags).
+ * Stream-ordered: returns once the kernel is enqueued on the context's stream
+ * (rt_assemble_bands waits for it). */
 int rt_assemble_bands_ex(rt_ctx *ctx, const void *d_gathered, int32_t resolution_x,
                          int32_t resolution_y, int32_t band_count, int32_t band_rows,
                          int32_t pixel_bytes, void *d_image);
+
+/* Waits for all work enqueued on the context's stream. */
+int rt_synchronize(rt_ctx *ctx);
 
 /* Batch closest-hit query: Scene.IntersectRay (Scene.cs:43-122) for n host
  * rays; writes n host rt_hit records. */

@@ -202,6 +202,7 @@ SIGNATURES = {
     "rt_assemble_bands": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_pixel_bytes": (C.c_int32, [C.c_int32]),
     "rt_finish": (C.c_int, [_P, C.POINTER(rt_stats)]),
+    "rt_synchronize": (C.c_int, [_P]),
     "rt_assemble_bands_ex": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_intersect_rays": (C.c_int, [_P, _P, C.c_int32, _P]),
 }

@@ -1213,7 +1213,9 @@ int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane 
 
 int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x, int32_t resolution_y,
                       int32_t band_count, int32_t band_rows, float *d_image) {
-    return rt_assemble_bands_ex(ctx, d_gathered, resolution_x, resolution_y, band_count, band_rows, 16, d_image);
+    const int st = rt_assemble_bands_ex(ctx, d_gathered, resolution_x, resolution_y, band_count, band_rows, 16,
+                                        d_image);
+    return st ? st : rt_synchronize(ctx);
 }
 
 int32_t rt_pixel_bytes(int32_t flags) {
@@ -1231,6 +1233,12 @@ int rt_assemble_bands_ex(rt_ctx *ctx, const void *d_gathered, int32_t resolution
     const int local = band_local_rows(resolution_y, band_count, band_rows);
     HIP_OR_FAIL(ctx, rtk::launch_assemble(d_gathered, resolution_x, resolution_y, band_count, band_rows, local,
                                           pixel_bytes, d_image, ctx->stream));
+    return RT_OK;  // stream-ordered: rt_synchronize (or the stream) before reading d_image elsewhere
+}
+
+int rt_synchronize(rt_ctx *ctx) {
+    if (!ctx) return RT_E_INVALID;
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     return RT_OK;
 }

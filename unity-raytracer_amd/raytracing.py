@@ -142,10 +142,12 @@ class Context:
                                        out.ctypes.data_as(C.c_void_p), C.byref(stats)))
         return out, stats
 
-    def render_device(self, camera: CameraData, plane: ImagePlane, params: abi.rt_render_params,
-                      dev_ptr: int, nbytes: int):
+    def render_device(self, camera, plane, params: abi.rt_render_params, dev_ptr: int, nbytes: int):
+        """camera / plane: CameraData / ImagePlane, or prebuilt rt_camera /
+        rt_image_plane structs (a frame loop builds them once)."""
         stats = abi.rt_stats()
-        cam, pl = camera_struct(camera), plane_struct(plane)
+        cam = camera if isinstance(camera, abi.rt_camera) else camera_struct(camera)
+        pl = plane if isinstance(plane, abi.rt_image_plane) else plane_struct(plane)
         self._check(self.lib.rt_render_device(self.h, C.byref(cam), C.byref(pl), C.byref(params),
                                               C.c_void_p(dev_ptr), C.c_size_t(nbytes), C.byref(stats)))
         return stats
@@ -157,9 +159,13 @@ class Context:
         return stats
 
     def assemble_bands(self, gathered_ptr: int, res_x: int, res_y: int, band_count: int,
-                       band_rows: int, image_ptr: int, pixel_bytes: int = 16):
+                       band_rows: int, image_ptr: int, pixel_bytes: int = 16, sync: bool = True):
+        """Reassemble gathered shards (device pointers); sync=False leaves the
+        kernel stream-ordered on the context's stream."""
         self._check(self.lib.rt_assemble_bands_ex(self.h, C.c_void_p(gathered_ptr), res_x, res_y,
                                                   band_count, band_rows, pixel_bytes, C.c_void_p(image_ptr)))
+        if sync:
+            self._check(self.lib.rt_synchronize(self.h))
 
     def intersect_rays(self, rays: np.ndarray) -> np.ndarray:
         """Scene.IntersectRay (Scene.cs:43-122) for (N, 6) float32 rays;
