@@ -15,6 +15,15 @@ import torch  # noqa: E402,F401
 import _rt_pkg  # noqa: E402
 
 
+def seg_per_wave(st):
+    """RT_SEG_PROFILE words -> per-wave averages (64-sample waves)."""
+    w = max(1, -(-st.primary_rays // 64))
+    v = st.box_tests
+    return {"waves": w, "nodes": round((v & 0xffffffff) / w, 2), "leaves": round((v >> 32) / w, 2),
+            "prim_cyc": round(st.triangle_tests / w), "shadow_cyc": round(st.sphere_tests / w),
+            "total_cyc": round(st.shading_fetches / w)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
@@ -25,6 +34,7 @@ def main():
     ap.add_argument("--res", default="")
     ap.add_argument("--bounces", type=int, default=-99)
     ap.add_argument("--no-lights", action="store_true")
+    ap.add_argument("--band", default="", help="i/n: render only row band i of n (8-row blocks): a light load")
     a = ap.parse_args()
     rt = _rt_pkg.load()
     fr = rt.make(a.config)
@@ -48,8 +58,12 @@ def main():
         for mode in a.modes.split(","):
             flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET,
                      "rowmajor": rt.abi.RT_FLAG_ROW_ORDER}.get(mode, 0)
-            p = rt.frame_params(fr, flags=flags)
-            cst = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=flags | 1), out.data_ptr(),
+            bkw = {}
+            if a.band:
+                bi, bn = map(int, a.band.split("/"))
+                bkw = dict(band_index=bi, band_count=bn, band_rows=8)
+            p = rt.frame_params(fr, flags=flags, **bkw)
+            cst = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=flags | 1, **bkw), out.data_ptr(),
                                     out.numel() * 4)
             img = out.cpu()
             same = None if ref is None else bool(torch.equal(img.view(torch.int32), ref.view(torch.int32)))
@@ -70,7 +84,12 @@ def main():
                               "total_ms": round(statistics.median(ts), 4), "Mrays_s": round(rays / km / 1e3, 1),
                               "rays": rays, "box": cst.box_tests, "tri": cst.triangle_tests,
                               "sph": cst.sphere_tests, "same_as_first": same,
-                              "same_as_base": same_base}), flush=True)
+                              "same_as_base": same_base,
+                              # RT_SEG_PROFILE builds: summed per-wave shader clocks (setup, camera packet,
+                              # first shadow packet, whole tile) in the test-counter words of a timed frame
+                              **({"seg_cycles": [st.box_tests, st.triangle_tests, st.sphere_tests,
+                                                 st.shading_fetches],
+                                  "seg_per_wave": seg_per_wave(st)} if "seg" in v else {})}), flush=True)
         ctx.close()
 
 

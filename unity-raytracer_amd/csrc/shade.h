@@ -137,11 +137,15 @@ __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, 
 }
 
 // Slot (tile, lane) -> pixel; false for lanes outside the image/shard.
+// `half` selects the slot set of a pair wave (64 * 2 samples per tile): half
+// h holds pixels [h * ppw, (h + 1) * ppw) of the tile, ppw = 64 / spp, so a
+// pixel's samples always sit in consecutive lanes of one slot set.
 __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int lane, int &px, int &ly, int &gy,
-                                           int &s) {
+                                           int &s, int half = 0) {
     const int spp = F.spp;
-    const int pix = lane / spp;
-    s = lane - pix * spp;
+    const int lp = lane / spp;
+    const int pix = half * (rtd::kWaveSize / spp) + lp;
+    s = lane - lp * spp;
     const int tx = tile % F.tiles_x, ty = tile / F.tiles_x;
     px = tx * F.tile_w + pix % F.tile_w;
     ly = ty * F.tile_h + pix / F.tile_w;
@@ -150,7 +154,8 @@ __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int
         const int blk = ly / F.band_rows;
         gy = (blk * F.band_count + F.band_index) * F.band_rows + (ly - blk * F.band_rows);
     }
-    return pix < F.tile_w * F.tile_h && px < F.res_x && ly < F.local_rows && gy < F.res_y;
+    return lp < rtd::kWaveSize / spp && pix < F.tile_w * F.tile_h && px < F.res_x && ly < F.local_rows &&
+           gy < F.res_y;
 }
 
 }  // namespace rts

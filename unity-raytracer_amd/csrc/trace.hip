@@ -50,31 +50,34 @@ namespace {
 #define RT_MK_PACKET_DEPTHS 1
 #endif
 
+// RT_SEG_PROFILE (profiling builds only): per-wave shader-clock time of the
+// setup / camera-packet / first-level shadow-packet segments and the whole
+// tile, summed into the (otherwise unused, non-counting) test-counter words.
+#ifdef RT_SEG_PROFILE
+#define RT_SEG(x) x
+#else
+#define RT_SEG(x)
+#endif
+struct SegClock {
+    unsigned long long setup, prim, shadow, visits;
+};
+
+// Shade levels depth0.. of one sample with per-lane traversal: the mirror
+// recursion unrolled into a loop, its results folded back to front so
+// c + km*(c' + km'*(...)) rounds exactly like the reference.
 template <bool COUNT>
-__device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
-                                         int *wstack, Counts &cnt) {
+__device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F, f3 o, f3 d, int depth0,
+                                           const rtt::Stack &st, Counts &cnt) {
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
-    int depth = 0;
+    int depth = depth0;
     f3 term;
     while (true) {
         rtt::RayCtx r;
         rtt::setup_ray(r, o, d);
         float bt;
         int br;
-        bool hit;
-        // packets walk 4-wide nodes; the counting launch (bench.py's
-        // algorithmic-byte model) keeps the per-ray traversal's canonical counts
-        if (!COUNT && RT_MK_PACKET_PRIMARY && depth < RT_MK_PACKET_DEPTHS && S.bvh4) {
-            rtp::PacketLane P;
-            rtp::packet_trace<false, COUNT>(S, r, true, 0.0f, 0.0f, P, wstack, cnt);
-            bt = P.best_t;
-            br = P.best_rank;
-            hit = br >= 0;
-        } else {
-            hit = rtt::traverse<false, COUNT>(S, r, 0.0f, 0.0f, bt, br, st, cnt);
-        }
-        if (!hit) {  // :310-311
+        if (!rtt::traverse<false, COUNT>(S, r, 0.0f, 0.0f, bt, br, st, cnt)) {  // :310-311
             term = rtt::ld3(F.bg255);
             break;
         }
@@ -88,19 +91,13 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
             rtt::setup_ray(rs, sr.o, sr.dir);
             float dt;
             int dr;
-            if (!COUNT && RT_MK_PACKET_SHADOW && depth < RT_MK_PACKET_DEPTHS && S.bvh4) {
-                rtp::PacketLane Q;
-                rtp::packet_trace<true, COUNT>(S, rs, true, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
-                if (Q.best_rank == 1) continue;
-            } else if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) {
-                continue;
-            }
+            if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) continue;
             col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
         }
         const DevMaterial m = S.mats[sf.mat];
         if (m.ka_mirror.w != 0.0f && depth < F.max_bounces) {  // :358-363
-            fold_c[depth][0] = col.x; fold_c[depth][1] = col.y; fold_c[depth][2] = col.z;
-            fold_k[depth][0] = m.km.x; fold_k[depth][1] = m.km.y; fold_k[depth][2] = m.km.z;
+            fold_c[depth - depth0][0] = col.x; fold_c[depth - depth0][1] = col.y; fold_c[depth - depth0][2] = col.z;
+            fold_k[depth - depth0][0] = m.km.x; fold_k[depth - depth0][1] = m.km.y; fold_k[depth - depth0][2] = m.km.z;
             rts::reflect(sf, o, d);
             ++depth;
             cnt.reflection++;
@@ -109,10 +106,54 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         term = col;
         break;
     }
-    for (int k = depth - 1; k >= 0; --k) {
+    for (int k = depth - depth0 - 1; k >= 0; --k)
         term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
-    }
     return term;
+}
+
+
+// Shade (RayTracingSetup.cs:304-366) of one camera sample.  The first hit is
+// traced and shaded with wave packets (camera rays of a tile, then their
+// shadow rays to each light: packet.h, scalar node fetches); the mirror
+// chain below it (a few percent of samples) runs per lane (shade_levels).
+// The counting launch keeps the per-ray traversal's canonical counts.
+template <bool COUNT>
+__device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
+                                         int *wstack, Counts &cnt, SegClock &sg) {
+    (void)sg;
+    if (COUNT || !S.bvh4) return shade_levels<COUNT>(S, F, o, d, 0, st, cnt);
+    RT_SEG(const unsigned long long tq0 = __builtin_amdgcn_s_memtime();)
+    rtt::RayCtx r;
+    rtt::setup_ray(r, o, d);
+    rtp::PacketLane P;
+    rtp::packet_trace<false, COUNT>(S, r, true, 0.0f, 0.0f, P, wstack, cnt);
+    RT_SEG(sg.visits += P.nodes + ((unsigned long long)P.leaves << 32);
+           const unsigned long long tq1 = __builtin_amdgcn_s_memtime(); sg.setup = tq0; sg.prim = tq1 - tq0;)
+    if (P.best_rank < 0) return rtt::ld3(F.bg255);  // :310-311
+    const rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
+    f3 col = rts::ambient(S, S.mats[sf.mat]);
+    for (int l = 0; l < S.num_lights; ++l) {  // :327-356
+        const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
+        cnt.shadow++;
+        rtt::RayCtx rs;
+        rtt::setup_ray(rs, sr.o, sr.dir);
+        rtp::PacketLane Q;
+        RT_SEG(const unsigned long long tw0 = __builtin_amdgcn_s_memtime();)
+        rtp::packet_trace<true, COUNT>(S, rs, true, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
+        RT_SEG(sg.shadow += __builtin_amdgcn_s_memtime() - tw0;
+               sg.visits += Q.nodes + ((unsigned long long)Q.leaves << 32);)
+        if (Q.best_rank == 1) continue;
+        col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+    }
+    const DevMaterial m = S.mats[sf.mat];
+    if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363
+        cnt.reflection++;
+        f3 ro, rd;
+        rts::reflect(sf, ro, rd);
+        const f3 below = shade_levels<COUNT>(S, F, ro, rd, 1, st, cnt);
+        return col + mk(m.km.x, m.km.y, m.km.z) * below;
+    }
+    return col;
 }
 
 #ifndef RT_MK_MIN_WAVES
@@ -132,7 +173,7 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // samples in row-major sample order ((s0 + s1) + s2) + ..., store.
 template <bool COUNT>
 __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
-                                            int *wstack, int tile, int lane, Counts &cnt) {
+                                            int *wstack, int tile, int lane, Counts &cnt, SegClock &sg) {
     int px, ly, gy, s;
     const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
     f3 color = mk(0.0f, 0.0f, 0.0f);
@@ -140,14 +181,19 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
         f3 o, d;
         rts::primary_ray(F, px, gy, s, o, d);
         cnt.primary += 1;
-        color = shade_path<COUNT>(S, F, o, d, st, wstack, cnt);
+        color = shade_path<COUNT>(S, F, o, d, st, wstack, cnt, sg);
     }
     f3 sum = color;
     for (int k = 1; k < F.spp; ++k) {
         const int src = lane + k;
         sum = sum + mk(__shfl(color.x, src), __shfl(color.y, src), __shfl(color.z, src));
     }
-    if (active && s == 0) {
+    // the slot -> pixel mapping is recomputed from the (scalar) tile index
+    // rather than kept live across the trace, where it would be spilled
+    int tile2 = __builtin_amdgcn_readfirstlane(tile);
+    asm volatile("" : "+s"(tile2));
+    const bool active2 = rts::slot_pixel(F, tile2, lane, px, ly, gy, s);
+    if (active2 && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
         rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
@@ -168,9 +214,31 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     const int wid = blockIdx.x * kMkWaves + wave;
     if (wid >= F.num_tiles) return;  // wave-uniform
     // dispatch order: the previous frame's most expensive tiles first (F.tile_order)
-    const int tile = F.tile_order ? F.tile_order[wid] : wid;
+    const int tile = F.tile_order ? rtt::cload(F.tile_order + wid) : wid;  // scalar load: tile math stays SALU
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
-    render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt);
+    SegClock sg = {0ull, 0ull, 0ull, 0ull};
+    RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
+    render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt, sg);
+#ifdef RT_SEG_PROFILE
+    if (!COUNT) {
+        const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
+        // the lanes' copies are equal (uniform clocks); lane 0 may be idle, take the max
+        unsigned long long su = sg.setup ? sg.setup - ts0 : 0ull, pr = sg.prim, sh = sg.shadow, vi = sg.visits;
+        for (int off = 32; off > 0; off >>= 1) {
+            su = max(su, (unsigned long long)__shfl_xor((long long)su, off));
+            pr = max(pr, (unsigned long long)__shfl_xor((long long)pr, off));
+            sh = max(sh, (unsigned long long)__shfl_xor((long long)sh, off));
+            vi = max(vi, (unsigned long long)__shfl_xor((long long)vi, off));
+        }
+        if (lane == 0) {
+            unsigned long long *ctr = F.counters + (size_t)(blockIdx.x % kCounterSlots) * kCounterWords;
+            atomicAdd(ctr + 3, vi);  // packet visits: internal | leaves << 32 (setup clock su unused)
+            atomicAdd(ctr + 4, pr);
+            atomicAdd(ctr + 5, sh);
+            atomicAdd(ctr + 6, ts1 - ts0);
+        }
+    }
+#endif
     if (F.tile_cost && lane == 0) {
         // log-scale cost key (4 mantissa bits, < 512): one cheap sort pass set
         const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
@@ -178,6 +246,120 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
         F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
     }
     rtt::flush_counts<COUNT>(cnt, F.counters);
+}
+
+#ifndef RT_PAIR_MIN_WAVES
+#define RT_PAIR_MIN_WAVES 4
+#endif
+
+// Pair megakernel: one wave = one tile of 2 x 64 samples, two per lane
+// (slot sets h = 0, 1; rts::slot_pixel).  The first hit of both and their
+// shadow rays are traced together as wave packets (packet_trace_n<.., 2>),
+// so every node/leaf fetch and ordering step serves 128 rays; the mirror
+// chains below (a few percent of samples) run per lane, slot by slot.
+// Arithmetic per sample is exactly render_kernel's.
+__global__ __launch_bounds__(kWaveSize, RT_PAIR_MIN_WAVES) void render_pair_kernel(SceneDev S, FrameDev F) {
+    constexpr int N = 2;
+    __shared__ int stack_mem[kStackSize * kWaveSize];
+    __shared__ int wstack_mem[rtp::kWaveStack];
+    const int lane = threadIdx.x & 63;
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem + lane, ovf};
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    const int wid = blockIdx.x;
+    if (wid >= F.num_tiles) return;
+    const int tile = F.tile_order ? rtt::cload(F.tile_order + wid) : wid;
+    const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
+    bool act[N];
+    rtt::RayCtx r[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        int px, ly, gy, s;
+        act[j] = rts::slot_pixel(F, tile, lane, px, ly, gy, s, j);
+        f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+        if (act[j]) {
+            rts::primary_ray(F, px, gy, s, o, d);
+            cnt.primary++;
+        }
+        rtt::setup_ray(r[j], o, d);
+    }
+    rtp::PacketLane P[N];
+    {
+        const float zero[N] = {0.0f, 0.0f};
+        rtp::packet_trace_n<false, false, N>(S, r, act, zero, zero, P, wstack_mem, cnt);
+    }
+    bool hit[N];
+    rts::Surface sf[N];
+    f3 col[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        hit[j] = act[j] && P[j].best_rank >= 0;
+        col[j] = mk(0.0f, 0.0f, 0.0f);
+        if (hit[j]) {
+            sf[j] = rts::surface(S, r[j].o, r[j].d, P[j].best_t, P[j].best_rank);
+            col[j] = rts::ambient(S, S.mats[sf[j].mat]);
+        } else {
+            sf[j].p = sf[j].n = sf[j].view = mk(0.0f, 0.0f, 1.0f);
+            sf[j].mat = 0;
+        }
+    }
+    for (int l = 0; l < S.num_lights; ++l) {  // :327-356, wave-uniform
+        const DevLight Lt = S.lights[l];
+        rts::ShadowRay sr[N];
+        rtt::RayCtx rs[N];
+        float tl[N], d2[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            sr[j] = rts::shadow_ray(sf[j], Lt);
+            if (hit[j]) cnt.shadow++;
+            rtt::setup_ray(rs[j], sr[j].o, sr[j].dir);
+            tl[j] = sqrtf(sr[j].d2) * 1.001f;
+            d2[j] = sr[j].d2;
+        }
+        rtp::PacketLane Q[N];
+        rtp::packet_trace_n<true, false, N>(S, rs, hit, tl, d2, Q, wstack_mem, cnt);
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+            if (hit[j] && Q[j].best_rank != 1) col[j] = col[j] + rts::light_term(S, sf[j], S.mats[sf[j].mat], Lt, sr[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        f3 term = mk(0.0f, 0.0f, 0.0f);
+        if (act[j]) {
+            if (!hit[j]) {
+                term = rtt::ld3(F.bg255);  // :310-311
+            } else {
+                const DevMaterial m = S.mats[sf[j].mat];
+                term = col[j];
+                if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363
+                    cnt.reflection++;
+                    f3 ro, rd;
+                    rts::reflect(sf[j], ro, rd);
+                    const f3 below = shade_levels<false>(S, F, ro, rd, 1, st, cnt);
+                    term = col[j] + mk(m.km.x, m.km.y, m.km.z) * below;
+                }
+            }
+        }
+        f3 sum = term;
+        for (int k = 1; k < F.spp; ++k) {
+            const int src = lane + k;
+            sum = sum + mk(__shfl(term.x, src), __shfl(term.y, src), __shfl(term.z, src));
+        }
+        int tile2 = __builtin_amdgcn_readfirstlane(tile);
+        asm volatile("" : "+s"(tile2));
+        int px, ly, gy, s;
+        if (rts::slot_pixel(F, tile2, lane, px, ly, gy, s, j) && s == 0) {
+            f3 v = sum;
+            if (F.spp > 1) v = v / (float)F.spp;
+            rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+        }
+    }
+    if (F.tile_cost && lane == 0) {
+        const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
+        const unsigned e = c ? 31u - __clz(c) : 0u;
+        F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
+    }
+    rtt::flush_counts<false>(cnt, F.counters);
 }
 
 // Wave-synchronous megakernel: the Whitted chain advances level by level for
@@ -325,6 +507,8 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
     const int blocks = (F.num_tiles + kMkWaves - 1) / kMkWaves;
     if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+    else if (F.slots_per_lane == 2)
+        hipLaunchKernelGGL(render_pair_kernel, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S, F);
     else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     return hipGetLastError();

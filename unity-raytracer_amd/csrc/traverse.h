@@ -286,6 +286,19 @@ __device__ __forceinline__ float child_key(float lx, float hx, float ly, float h
     return tn <= tf ? tn : INFINITY;
 }
 
+// child_key with the near/far planes already chosen by the ray's direction
+// signs (near = lo for a positive inverse direction): max/min of the same
+// plane distances, so the same result in fewer instructions.
+__device__ __forceinline__ float child_key_nf(float nx, float fx, float ny, float fy, float nz, float fz,
+                                              const RayCtx &r, float tcull) {
+    const f3 noi = r.noi();
+    const float an = fmaf(nx, r.ninv.x, -noi.x), af = fmaf(fx, r.ninv.x, -noi.x);
+    const float bn = fmaf(ny, r.ninv.y, -noi.y), bf = fmaf(fy, r.ninv.y, -noi.y);
+    const float cn = fmaf(nz, r.ninv.z, -noi.z), cf = fmaf(fz, r.ninv.z, -noi.z);
+    const float tn = fmaxf(fmaxf(fmaxf(an, bn), cn), 0.0f);
+    const float tf = fminf(fminf(fminf(af, bf), cf), tcull);
+    return tn <= tf ? tn : INFINITY;
+}
 
 #define RT_CSWAP(i, j)                          \
     do {                                        \
