@@ -1,0 +1,64 @@
+"""Device-math shortcuts must be bit-identical to the IEEE operations they
+replace (DESIGN.md "Arithmetic contract"):
+
+* rtm::rcp_cr — v_rcp_f32 + Newton step + Markstein correction for
+  2^-125 < |b| < 2^125 — against IEEE 1.0f / b, EVERY float in that range
+  (both signs, ~4.2e9 values, counted on the device);
+* rts::spec_pow_int — binary powering in double with a Ziv rounding test,
+  falling back to the double pow — against the host's correctly rounded
+  pow((double)x, (double)y) rounded to float (numpy float64 power).
+Both run through librt_selftest.so (test infrastructure, not the product ABI).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "unity-raytracer_amd", "lib", "librt_selftest.so")
+
+
+@pytest.fixture(scope="module")
+def st(rt):
+    lib = C.CDLL(LIB)
+    lib.rt_selftest_rcp.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
+    lib.rt_selftest_rcp.restype = C.c_longlong
+    lib.rt_selftest_pow.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    lib.rt_selftest_pow.restype = C.c_int
+    return lib
+
+
+def test_rcp_exhaustive(st):
+    first = C.c_uint32(0)
+    # bit patterns of 2^-125 (exclusive) .. 2^125 (exclusive), both signs
+    bad = st.rt_selftest_rcp(0x01000001, 0x7E000000, C.byref(first))
+    assert bad == 0, f"{bad} mismatches, first at bits {first.value:#010x}"
+
+
+def _pow_dev(st, x, y):
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(y, np.float32)
+    out = np.empty_like(x)
+    assert st.rt_selftest_pow(x.ctypes.data, y.ctypes.data, out.ctypes.data, x.size) == 0
+    return out
+
+
+def test_spec_pow_matches_host_pow(st):
+    rng = np.random.default_rng(20250101)
+    n = 1 << 20
+    # x: every binade of [0, 1] (random bit patterns) plus edge values
+    x = rng.integers(0, 0x3F800001, n, dtype=np.uint32).view(np.float32)
+    x[:8] = np.array([0.0, -0.0, 1.0, 0.5, 1e-45, 1e-38, 0.999999940, 0.9999], np.float32)
+    exps = np.concatenate([np.arange(1, 129), [0.0, 0.5, 2.5, 129.0, 200.0, 1000.0, -1.0, 3.25]]).astype(np.float32)
+    y = exps[rng.integers(0, exps.size, n)]
+    y[:8] = 8.0
+    got = _pow_dev(st, x, y)
+    with np.errstate(all="ignore"):
+        want = np.power(x.astype(np.float64), y.astype(np.float64)).astype(np.float32)
+    diff = got.view(np.uint32) != want.view(np.uint32)
+    both_nan = np.isnan(got) & np.isnan(want)
+    bad = np.flatnonzero(diff & ~both_nan)
+    assert bad.size == 0, f"{bad.size} mismatches, e.g. x={x[bad[0]]!r} y={y[bad[0]]!r}: {got[bad[0]]!r} vs {want[bad[0]]!r}"

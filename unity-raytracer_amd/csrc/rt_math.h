@@ -33,6 +33,43 @@ RT_HD f3 operator*(float s, f3 a) { return mk(s * a.x, s * a.y, s * a.z); }
 RT_HD f3 operator/(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 RT_HD f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
 
+// min/max inside the slab test.  Unity's min/max ignore a NaN operand, as
+// fminf/fmaxf do; the two can differ only in which zero they return for
+// (-0, +0), and a slab test's outcome (tmin <= tmax) cannot tell the zeros
+// apart — so on the device the single-instruction v_min/v_max_f32 are used.
+#ifndef RT_SLAB_FMIN
+#define RT_SLAB_FMIN 1
+#endif
+#ifndef RT_RCP_FAST
+#define RT_RCP_FAST 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && RT_SLAB_FMIN
+__device__ __forceinline__ float slab_min(float x, float y) { return fminf(x, y); }
+__device__ __forceinline__ float slab_max(float x, float y) { return fmaxf(x, y); }
+#else
+RT_HD float slab_min(float x, float y) { return (__builtin_isnan(y) || x < y) ? x : y; }
+RT_HD float slab_max(float x, float y) { return (__builtin_isnan(y) || x > y) ? x : y; }
+#endif
+
+// Correctly rounded 1.0f / b.  On the device, for 2^-125 < |b| < 2^125 (no
+// operand or result scaling needed) the hardware division sequence without
+// its scale/fixup steps: v_rcp_f32, one Newton step, one Markstein
+// correction (verified bit-exact against IEEE division for every float in
+// that range: tests/test_gpu_math.py); other b take the IEEE division.
+#if defined(__HIP_DEVICE_COMPILE__) && RT_RCP_FAST
+__device__ __forceinline__ float rcp_cr(float b) {
+    const float ab = fabsf(b);
+    if (__builtin_expect(!(ab > 0x1p-125f && ab < 0x1p125f), 0)) return 1.0f / b;
+    const float y = __builtin_amdgcn_rcpf(b);
+    const float e = fmaf(-b, y, 1.0f);
+    const float y1 = fmaf(e, y, y);
+    const float r = fmaf(-b, y1, 1.0f);
+    return fmaf(r, y1, y1);
+}
+#else
+RT_HD float rcp_cr(float b) { return 1.0f / b; }
+#endif
+
 RT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RT_HD f3 cross(f3 x, f3 y) {
     return mk(x.y * y.z - x.z * y.y, x.z * y.x - x.x * y.z, x.x * y.y - x.y * y.x);
@@ -40,11 +77,13 @@ RT_HD f3 cross(f3 x, f3 y) {
 RT_HD float lengthsq(f3 a) { return dot(a, a); }
 RT_HD float length(f3 a) { return sqrtf(dot(a, a)); }
 RT_HD f3 normalize(f3 a) {
-    float r = 1.0f / sqrtf(dot(a, a));
+    float r = rcp_cr(sqrtf(dot(a, a)));
     return r * a;
 }
 RT_HD float umin(float x, float y) { return (__builtin_isnan(y) || x < y) ? x : y; }
 RT_HD float umax(float x, float y) { return (__builtin_isnan(y) || x > y) ? x : y; }
+
+
 
 // RMath.Epsilon (RMath.cs:9) and RayTracingSetup.ShadowRayEpsilon (:42)
 constexpr float kEpsilon = 0.00001f;
@@ -57,14 +96,14 @@ RT_HD bool ref_slab(f3 o, f3 inv, f3 lo, f3 hi) {
     float tmin = 0.0f, tmax = INFINITY;
     float t1, t2;
     t1 = (lo.x - o.x) * inv.x; t2 = (hi.x - o.x) * inv.x;
-    tmin = umin(umax(t1, tmin), umax(t2, tmin));
-    tmax = umax(umin(t1, tmax), umin(t2, tmax));
+    tmin = slab_min(slab_max(t1, tmin), slab_max(t2, tmin));
+    tmax = slab_max(slab_min(t1, tmax), slab_min(t2, tmax));
     t1 = (lo.y - o.y) * inv.y; t2 = (hi.y - o.y) * inv.y;
-    tmin = umin(umax(t1, tmin), umax(t2, tmin));
-    tmax = umax(umin(t1, tmax), umin(t2, tmax));
+    tmin = slab_min(slab_max(t1, tmin), slab_max(t2, tmin));
+    tmax = slab_max(slab_min(t1, tmax), slab_min(t2, tmax));
     t1 = (lo.z - o.z) * inv.z; t2 = (hi.z - o.z) * inv.z;
-    tmin = umin(umax(t1, tmin), umax(t2, tmin));
-    tmax = umax(umin(t1, tmax), umin(t2, tmax));
+    tmin = slab_min(slab_max(t1, tmin), slab_max(t2, tmin));
+    tmax = slab_max(slab_min(t1, tmax), slab_min(t2, tmax));
     return tmin <= tmax;
 }
 
@@ -76,7 +115,7 @@ RT_HD bool ref_triangle(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float &t_out) {
     if (a > -kEpsilon && a < kEpsilon) return false;
     f3 s = o - v0;
     const float sh = dot(s, h);
-    float f = 1.0f / a;
+    float f = rcp_cr(a);
     float u = f * sh;
     if (u < 0.0f || u > 1.0f) return false;
     f3 q = cross(s, e1);

@@ -68,6 +68,32 @@ __device__ __attribute__((noinline)) float spec_pow(float x, float y) { return (
 __device__ __forceinline__ float spec_pow(float x, float y) { return (float)pow((double)x, (double)y); }
 #endif
 
+// (float)Math.Pow((double)x, (double)y) for the Phong exponents scenes use:
+// for an integer y in [1, 128], x^y by binary powering in double (relative
+// error below 2y * 2^-53; no under-/overflow can matter since 0 <= x <= 1 and
+// the float result of anything below 2^-1000 is 0), rounded to float when
+// that error bound cannot straddle a float rounding boundary (Ziv's test):
+// then the result is the float nearest the exact power — which is what the
+// host's correctly rounded pow, rounded to float, also is.  Otherwise, and
+// for any other exponent, the out-of-line double pow.
+#ifndef RT_POW_INT
+#define RT_POW_INT 1
+#endif
+__device__ __forceinline__ float spec_pow_int(float x, float y) {
+    const int n = (int)y;
+    if (RT_POW_INT && (float)n == y && n >= 1 && n <= 128) {
+        double b = (double)x, r = (n & 1) ? b : 1.0;
+        for (int e = n >> 1; e; e >>= 1) {
+            b = b * b;
+            if (e & 1) r = r * b;
+        }
+        const double err = fabs(r) * ((double)(2 * n) * 0x1p-53);
+        const float lo = (float)(r - err), hi = (float)(r + err);
+        if (lo == hi && (r != 0.0 || err == 0.0)) return (float)r;
+    }
+    return spec_pow(x, y);
+}
+
 // diffuseRgb + specularRgb of one unoccluded light (:350-355).
 __device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &s, const rtd::DevMaterial &m,
                                          const rtd::DevLight &L, const ShadowRay &sr) {
@@ -84,7 +110,7 @@ __device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &
         // pow(float, float) = (float)System.Math.Pow((double)x, (double)y); a
         // material whose specular term is always a signed zero skips it
         // (ks.w, rt_abi.cpp to_dev): (ks * 0) * E has the same bits.
-        const float pw = m.ks.w != 0.0f ? 0.0f : spec_pow(cnh, m.kd_phong.w);
+        const float pw = m.ks.w != 0.0f ? 0.0f : spec_pow_int(cnh, m.kd_phong.w);
         spec = (mk(m.ks.x, m.ks.y, m.ks.z) * pw) * e;
     }
     return diffuse + spec;
@@ -108,6 +134,28 @@ __device__ __forceinline__ void primary_ray(const rtd::FrameDev &F, int px, int 
     const f3 pp = (rtt::ld3(F.top_left) + rm * rtt::ld3(F.right)) - rtt::ld3(F.up) * dm;
     o = rtt::ld3(F.cam_pos);
     d = rtm::normalize(pp - o);
+}
+
+// Sum of a pixel's samples in row-major sample order ((s0 + s1) + s2) + ...,
+// valid at the pixel's sample-0 lane (samples sit in consecutive lanes).  4
+// spp: DPP quad moves (no LDS round trip); otherwise lane shuffles.  Must be
+// called with every lane of the wave active.
+__device__ __forceinline__ rtm::f3 sample_sum(rtm::f3 c, int lane, int spp) {
+    rtm::f3 sum = c;
+    if (spp == 4) {
+        // quad_perm [k,k,k,k]: every lane of a quad reads the quad's lane k
+#define RT_QREAD(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), (ctrl), 0xf, 0xf, false))
+        sum = sum + rtm::mk(RT_QREAD(c.x, 0x55), RT_QREAD(c.y, 0x55), RT_QREAD(c.z, 0x55));
+        sum = sum + rtm::mk(RT_QREAD(c.x, 0xAA), RT_QREAD(c.y, 0xAA), RT_QREAD(c.z, 0xAA));
+        sum = sum + rtm::mk(RT_QREAD(c.x, 0xFF), RT_QREAD(c.y, 0xFF), RT_QREAD(c.z, 0xFF));
+#undef RT_QREAD
+        return sum;
+    }
+    for (int k = 1; k < spp; ++k) {
+        const int src = lane + k;
+        sum = sum + rtm::mk(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src));
+    }
+    return sum;
 }
 
 // Color -> Color32 (UnityEngine, restated): (byte)Mathf.Round(Mathf.Clamp01(c)

@@ -121,7 +121,9 @@ template <bool COUNT>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
                                          int *wstack, Counts &cnt, SegClock &sg) {
     (void)sg;
+#ifndef RT_EXP_NO_TAIL
     if (COUNT || !S.bvh4) return shade_levels<COUNT>(S, F, o, d, 0, st, cnt);
+#endif
     RT_SEG(const unsigned long long tq0 = __builtin_amdgcn_s_memtime();)
     rtt::RayCtx r;
     rtt::setup_ray(r, o, d);
@@ -150,7 +152,11 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         cnt.reflection++;
         f3 ro, rd;
         rts::reflect(sf, ro, rd);
+#ifdef RT_EXP_NO_TAIL
+        const f3 below = ro + rd;
+#else
         const f3 below = shade_levels<COUNT>(S, F, ro, rd, 1, st, cnt);
+#endif
         return col + mk(m.km.x, m.km.y, m.km.z) * below;
     }
     return col;
@@ -183,11 +189,7 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
         cnt.primary += 1;
         color = shade_path<COUNT>(S, F, o, d, st, wstack, cnt, sg);
     }
-    f3 sum = color;
-    for (int k = 1; k < F.spp; ++k) {
-        const int src = lane + k;
-        sum = sum + mk(__shfl(color.x, src), __shfl(color.y, src), __shfl(color.z, src));
-    }
+    const f3 sum = rts::sample_sum(color, lane, F.spp);
     // the slot -> pixel mapping is recomputed from the (scalar) tile index
     // rather than kept live across the trace, where it would be spilled
     int tile2 = __builtin_amdgcn_readfirstlane(tile);
@@ -340,11 +342,7 @@ __global__ __launch_bounds__(kWaveSize, RT_PAIR_MIN_WAVES) void render_pair_kern
                 }
             }
         }
-        f3 sum = term;
-        for (int k = 1; k < F.spp; ++k) {
-            const int src = lane + k;
-            sum = sum + mk(__shfl(term.x, src), __shfl(term.y, src), __shfl(term.z, src));
-        }
+        const f3 sum = rts::sample_sum(term, lane, F.spp);
         int tile2 = __builtin_amdgcn_readfirstlane(tile);
         asm volatile("" : "+s"(tile2));
         int px, ly, gy, s;
@@ -454,11 +452,7 @@ __global__ __launch_bounds__(kBlockThreads) void render_packet_kernel(SceneDev S
     for (int k = depth - 1; k >= 0; --k)
         term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
     const f3 color = term;
-    f3 sum = color;
-    for (int k = 1; k < F.spp; ++k) {
-        const int src = lane + k;
-        sum = sum + mk(__shfl(color.x, src), __shfl(color.y, src), __shfl(color.z, src));
-    }
+    const f3 sum = rts::sample_sum(color, lane, F.spp);
     if (active && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;

@@ -40,7 +40,7 @@ __device__ __forceinline__ void setup_ray(RayCtx &r, f3 o, f3 d) {
     r.d = d;
     r.ninv = mk(__builtin_amdgcn_rcpf(nudge(d.x)), __builtin_amdgcn_rcpf(nudge(d.y)),
                 __builtin_amdgcn_rcpf(nudge(d.z)));
-    r.inv_v = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.inv_v = mk(rtm::rcp_cr(d.x), rtm::rcp_cr(d.y), rtm::rcp_cr(d.z));
     r.noi_v = mk(o.x * r.ninv.x, o.y * r.ninv.y, o.z * r.ninv.z);
 }
 
@@ -406,7 +406,10 @@ __device__ __forceinline__ bool traverse(const rtd::SceneDev &S, const RayCtx &r
     return best_rank >= 0;
 }
 
+// Sum over the wave.  With every lane active (the kernels' epilogues) a DPP
+// reduction (no LDS round trips); otherwise cross-lane shuffles.
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
+    if (__ballot(1) == ~0ull) return __reduce_add_sync(~0ull, v);
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
 }
