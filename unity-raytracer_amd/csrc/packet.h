@@ -281,239 +281,4 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
 #undef RT_PK_PUSH
 }
 
-// ---------------------------------------------------------------------------
-// N rays per lane (the pair megakernel: a wave traces 64*N samples).  One
-// node or leaf fetch now serves N rays per lane: the node-visit latency chain
-// (scalar fetch -> box tests -> wave ordering -> next fetch) is paid once per
-// 64*N rays.  Every lane/slot keeps its own exact tests and winner, so the
-// answers equal packet_trace's and the brute-force reference's.
-
-template <bool ANY, bool COUNT, int N>
-__device__ __forceinline__ void packet_leaf_tris_n(const rtd::SceneDev &S, const RayCtx *r, PacketLane *L,
-                                                   int &wgate, const float *d2, int first, int count, Counts &cnt) {
-    const rtd::TriRec *tb = S.tris + first;
-    const rtd::TriRec t0 = rtt::cload(tb);
-    const rtd::TriRec t1 = rtt::cload(tb + (count > 1 ? 1 : 0));
-    const int gate = uni(__float_as_int(t0.p2.z));
-    if (gate >= 0 && gate != wgate) {
-        const rtd::MeshGate g = rtt::cload(S.gates + gate);
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (L[j].live) {
-                L[j].gate_ok = rtm::ref_slab(r[j].o, r[j].inv(), mk(g.lo.x, g.lo.y, g.lo.z),
-                                             mk(g.hi.x, g.hi.y, g.hi.z));
-                L[j].gate_cached = gate;
-                if (COUNT) cnt.box++;
-            }
-        wgate = gate;
-    }
-    bool go[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) go[j] = L[j].live && (gate < 0 || L[j].gate_ok);
-#pragma unroll
-    for (int j = 0; j < N; ++j)
-        if (go[j] && packet_tri<ANY, COUNT>(r[j], L[j], d2[j], t0, cnt)) go[j] = L[j].live = false;
-    if (count > 1) {
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (go[j] && packet_tri<ANY, COUNT>(r[j], L[j], d2[j], t1, cnt)) go[j] = L[j].live = false;
-    }
-    if (count > 2) {
-        const rtd::TriRec t2 = rtt::cload(tb + 2);
-        const rtd::TriRec t3 = rtt::cload(tb + (count > 3 ? 3 : 2));
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (go[j] && packet_tri<ANY, COUNT>(r[j], L[j], d2[j], t2, cnt)) go[j] = L[j].live = false;
-        if (count > 3) {
-#pragma unroll
-            for (int j = 0; j < N; ++j)
-                if (go[j] && packet_tri<ANY, COUNT>(r[j], L[j], d2[j], t3, cnt)) go[j] = L[j].live = false;
-        }
-    }
-}
-
-template <bool ANY, bool COUNT, int N>
-__device__ __forceinline__ void packet_trace_n(const rtd::SceneDev &S, const RayCtx *r, const bool *part,
-                                               const float *tlimit, const float *d2, PacketLane *L, int *wstack,
-                                               Counts &cnt) {
-    unsigned long long any_live = 0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        L[j].best_t = FLT_MAX;
-        L[j].best_rank = -1;
-        L[j].tcull = ANY ? tlimit[j] : FLT_MAX;
-        L[j].gate_cached = -1;
-        L[j].gate_ok = false;
-#ifdef RT_SEG_PROFILE
-        L[j].nodes = 0;
-        L[j].leaves = 0;
-#endif
-        if (COUNT && part[j]) cnt.box++;
-        L[j].live = part[j] && S.has_prims &&
-                    rtm::ref_slab(r[j].o, r[j].inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi));
-        any_live |= __ballot(L[j].live);
-    }
-    if (any_live == 0) return;
-    int node = 0;    // wave-uniform
-    int sp = 0;      // wave-uniform
-    int wgate = -2;  // mesh whose gate every live lane has evaluated, wave-uniform
-    int topv = 0;    // cached top of the wave stack (see packet_trace)
-    // direction signs over every live ray of the wave
-    bool same_signs = true;
-    int sgn[3] = {0, 0, 0};
-    {
-        unsigned long long neg[3] = {0, 0, 0}, pos[3] = {0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            neg[0] |= __ballot(L[j].live && r[j].ninv.x < 0.0f);
-            neg[1] |= __ballot(L[j].live && r[j].ninv.y < 0.0f);
-            neg[2] |= __ballot(L[j].live && r[j].ninv.z < 0.0f);
-            pos[0] |= __ballot(L[j].live && !(r[j].ninv.x < 0.0f));
-            pos[1] |= __ballot(L[j].live && !(r[j].ninv.y < 0.0f));
-            pos[2] |= __ballot(L[j].live && !(r[j].ninv.z < 0.0f));
-        }
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            same_signs = same_signs && (neg[a] == 0 || pos[a] == 0);
-            sgn[a] = neg[a] != 0;
-        }
-    }
-    const int ox = uni(same_signs && sgn[0]), oy = uni(same_signs && sgn[1]), oz = uni(same_signs && sgn[2]);
-    while (true) {
-#ifdef RT_SEG_PROFILE
-        if (node >= 0) L[0].nodes++; else L[0].leaves++;
-#endif
-        if (node >= 0) {
-            float k[N][4];
-#pragma unroll
-            for (int j = 0; j < N; ++j) k[j][0] = k[j][1] = k[j][2] = k[j][3] = INFINITY;
-            const int4 ch = rtt::cload(&S.nodes4[node].child);
-            if (same_signs) {
-                const float4 *pl = reinterpret_cast<const float4 *>(S.nodes4 + node);
-                const float4 nx = rtt::cload(pl + ox), fx = rtt::cload(pl + (1 - ox));
-                const float4 ny = rtt::cload(pl + 2 + oy), fy = rtt::cload(pl + (3 - oy));
-                const float4 nz = rtt::cload(pl + 4 + oz), fz = rtt::cload(pl + (5 - oz));
-#pragma unroll
-                for (int j = 0; j < N; ++j)
-                    if (L[j].live) {
-                        k[j][0] = rtt::child_key_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r[j], L[j].tcull);
-                        k[j][1] = rtt::child_key_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r[j], L[j].tcull);
-                        k[j][2] = rtt::child_key_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r[j], L[j].tcull);
-                        k[j][3] = rtt::child_key_nf(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r[j], L[j].tcull);
-                        if (COUNT) cnt.box += 4;
-                    }
-            } else {
-                const rtd::BvhNode4 nd = rtt::cload(S.nodes4 + node);
-#pragma unroll
-                for (int j = 0; j < N; ++j)
-                    if (L[j].live) {
-                        k[j][0] = rtt::child_key(nd.lox.x, nd.hix.x, nd.loy.x, nd.hiy.x, nd.loz.x, nd.hiz.x, r[j],
-                                                 L[j].tcull);
-                        k[j][1] = rtt::child_key(nd.lox.y, nd.hix.y, nd.loy.y, nd.hiy.y, nd.loz.y, nd.hiz.y, r[j],
-                                                 L[j].tcull);
-                        k[j][2] = rtt::child_key(nd.lox.z, nd.hix.z, nd.loy.z, nd.hiy.z, nd.loz.z, nd.hiz.z, r[j],
-                                                 L[j].tcull);
-                        k[j][3] = rtt::child_key(nd.lox.w, nd.hix.w, nd.loy.w, nd.hiy.w, nd.loz.w, nd.hiz.w, r[j],
-                                                 L[j].tcull);
-                        if (COUNT) cnt.box += 4;
-                    }
-            }
-            // representative: the first live lane of the first slot that has one
-            int rep = -1, repj = 0;
-#pragma unroll
-            for (int j = N - 1; j >= 0; --j) {
-                const unsigned long long m = __ballot(L[j].live);
-                if (m) {
-                    rep = __ffsll((long long)m) - 1;
-                    repj = j;
-                }
-            }
-            unsigned q[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                bool need = false;
-                float kr = k[0][c];
-#pragma unroll
-                for (int j = 0; j < N; ++j) {
-                    need = need || k[j][c] != INFINITY;
-                    if (j > 0 && repj == j) kr = k[j][c];
-                }
-                const unsigned long long nm = __ballot(need);
-                const unsigned kb = (unsigned)__builtin_amdgcn_readlane(__float_as_int(kr), rep);
-                q[c] = nm == 0 ? kKeyNone : (kb != kKeyNone ? kb : 0x7f7fffffu);
-            }
-            unsigned q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-            int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-#define RT_PSWAP(i, j)                            \
-    do {                                          \
-        const bool sw_ = q##j < q##i;             \
-        const unsigned tq_ = sw_ ? q##j : q##i;   \
-        q##j = sw_ ? q##i : q##j;                 \
-        q##i = tq_;                               \
-        const int tc_ = sw_ ? c##j : c##i;        \
-        c##j = sw_ ? c##i : c##j;                 \
-        c##i = tc_;                               \
-    } while (0)
-            RT_PSWAP(0, 1);
-            RT_PSWAP(2, 3);
-            RT_PSWAP(0, 2);
-            RT_PSWAP(1, 3);
-            RT_PSWAP(1, 2);
-#undef RT_PSWAP
-#define RT_PK_PUSHN(v)                              \
-    do {                                            \
-        if (sp > 0) wstack[sp - 1] = topv;          \
-        topv = (v);                                 \
-        ++sp;                                       \
-    } while (0)
-            if (q0 != kKeyNone) {
-                if (q3 != kKeyNone) RT_PK_PUSHN(c3);
-                if (q2 != kKeyNone) RT_PK_PUSHN(c2);
-                if (q1 != kKeyNone) RT_PK_PUSHN(c1);
-                node = uni(c0);
-                continue;
-            }
-#undef RT_PK_PUSHN
-        } else {
-            const int v = ~node;
-            const int first = v & ((1 << rtd::kLeafFirstBits) - 1);
-            const int count = ((v >> rtd::kLeafFirstBits) & 3) + 1;
-            const int kind = (v >> (rtd::kLeafFirstBits + 2)) & 1;
-            if (kind == rtd::kLeafTri) {
-                packet_leaf_tris_n<ANY, COUNT, N>(S, r, L, wgate, d2, first, count, cnt);
-            } else {
-                const int gate = rtt::cload(&S.sphs[first].misc).y;
-#pragma unroll
-                for (int j = 0; j < N; ++j)
-                    if (L[j].live) {
-                        rtt::Trav t;
-                        t.best_t = L[j].best_t;
-                        t.best_rank = L[j].best_rank;
-                        t.tcull = L[j].tcull;
-                        t.gate_cached = L[j].gate_cached;
-                        t.gate_ok = L[j].gate_ok;
-                        const bool occ = rtt::leaf<ANY, COUNT, true>(S, r[j], t, d2[j], first, count, kind, gate, cnt);
-                        L[j].best_t = t.best_t;
-                        L[j].best_rank = t.best_rank;
-                        L[j].tcull = t.tcull;
-                        L[j].gate_cached = t.gate_cached;
-                        L[j].gate_ok = t.gate_ok;
-                        if (ANY && occ) L[j].live = false;
-                    }
-                if (gate >= 0) wgate = -2;
-            }
-            if (ANY) {
-                unsigned long long lv = 0;
-#pragma unroll
-                for (int j = 0; j < N; ++j) lv |= __ballot(L[j].live);
-                if (lv == 0) return;
-            }
-        }
-        if (sp == 0) return;
-        --sp;
-        node = uni(topv);
-        if (sp > 0) topv = wstack[sp - 1];
-    }
-}
-
 }  // namespace rtp

@@ -233,11 +233,6 @@ rtd::DevMaterial to_dev(const rt_material &m) {
     return d;
 }
 
-#ifndef RT_PAIR_TILES
-#define RT_PAIR_TILES 0
-#endif
-constexpr bool kPairTiles = RT_PAIR_TILES != 0;
-
 int isqrt_exact(int v) {
     if (v <= 0) return -1;
     int n = 1;
@@ -292,13 +287,9 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.band_count = band_count;
     F.band_rows = band_rows;
     F.local_rows = band_local_rows(F.res_y, band_count, band_rows);
-    // tile: 64/spp pixels per wave (the pair megakernel, the default
-    // non-counting megakernel path on a 4-wide BVH: twice that, two samples
-    // per lane); a power of two is laid out as a near-square 2^a x 2^b block
-    const bool pair_tiles = kPairTiles && ctx->S.bvh4 &&
-                            (prm->flags & (RT_FLAG_COUNT_TESTS | RT_FLAG_WAVEFRONT | RT_FLAG_PACKET)) == 0;
-    F.slots_per_lane = pair_tiles ? 2 : 1;
-    const int ppw = rtd::kWaveSize / F.spp * F.slots_per_lane;
+    // tile: 64/spp pixels per wave; a power of two is laid out as a
+    // near-square 2^a x 2^b block
+    const int ppw = rtd::kWaveSize / F.spp;
     int tw = ppw, th = 1;
     if ((ppw & (ppw - 1)) == 0) {
         int lg = 0;

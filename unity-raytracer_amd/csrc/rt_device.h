@@ -167,7 +167,6 @@ struct FrameDev {
     int local_rows;          // rows of the compact output buffer
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
-    int slots_per_lane;      // samples per lane of a megakernel tile: 1, or 2 (render_pair_kernel)
     void *out;               // local_rows x res_x pixels in out_format
     const int *tile_order;   // megakernel dispatch order (null: row-major)
     unsigned *tile_cost;     // per-tile cost of this frame (shader clock), null: not recorded

@@ -184,15 +184,13 @@ __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, 
     }
 }
 
-// Slot (tile, lane) -> pixel; false for lanes outside the image/shard.
-// `half` selects the slot set of a pair wave (64 * 2 samples per tile): half
-// h holds pixels [h * ppw, (h + 1) * ppw) of the tile, ppw = 64 / spp, so a
-// pixel's samples always sit in consecutive lanes of one slot set.
+// Slot (tile, lane) -> pixel; false for lanes outside the image/shard.  A
+// pixel's samples sit in consecutive lanes.
 __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int lane, int &px, int &ly, int &gy,
-                                           int &s, int half = 0) {
+                                           int &s) {
     const int spp = F.spp;
     const int lp = lane / spp;
-    const int pix = half * (rtd::kWaveSize / spp) + lp;
+    const int pix = lp;
     s = lane - lp * spp;
     const int tx = tile % F.tiles_x, ty = tile / F.tiles_x;
     px = tx * F.tile_w + pix % F.tile_w;

@@ -121,9 +121,7 @@ template <bool COUNT>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
                                          int *wstack, Counts &cnt, SegClock &sg) {
     (void)sg;
-#ifndef RT_EXP_NO_TAIL
     if (COUNT || !S.bvh4) return shade_levels<COUNT>(S, F, o, d, 0, st, cnt);
-#endif
     RT_SEG(const unsigned long long tq0 = __builtin_amdgcn_s_memtime();)
     rtt::RayCtx r;
     rtt::setup_ray(r, o, d);
@@ -152,11 +150,7 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         cnt.reflection++;
         f3 ro, rd;
         rts::reflect(sf, ro, rd);
-#ifdef RT_EXP_NO_TAIL
-        const f3 below = ro + rd;
-#else
         const f3 below = shade_levels<COUNT>(S, F, ro, rd, 1, st, cnt);
-#endif
         return col + mk(m.km.x, m.km.y, m.km.z) * below;
     }
     return col;
@@ -250,103 +244,93 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
 
-#ifndef RT_PAIR_MIN_WAVES
-#define RT_PAIR_MIN_WAVES 4
+#ifndef RT_LV_MIN_WAVES
+#define RT_LV_MIN_WAVES 6
 #endif
 
-// Pair megakernel: one wave = one tile of 2 x 64 samples, two per lane
-// (slot sets h = 0, 1; rts::slot_pixel).  The first hit of both and their
-// shadow rays are traced together as wave packets (packet_trace_n<.., 2>),
-// so every node/leaf fetch and ordering step serves 128 rays; the mirror
-// chains below (a few percent of samples) run per lane, slot by slot.
-// Arithmetic per sample is exactly render_kernel's.
-__global__ __launch_bounds__(kWaveSize, RT_PAIR_MIN_WAVES) void render_pair_kernel(SceneDev S, FrameDev F) {
-    constexpr int N = 2;
-    __shared__ int stack_mem[kStackSize * kWaveSize];
+// Level-synchronous all-packet megakernel (the default non-counting path on
+// a 4-wide BVH): one wave = one tile of 64 samples; the Whitted chain
+// advances level by level for the whole wave, and every level's rays — the
+// camera rays, the mirror rays of the lanes still bouncing, and each level's
+// shadow rays — are traced as wave packets (packet.h).  Without a per-lane
+// traversal the kernel needs no LDS lane stack and ~80 VGPRs (6 waves/SIMD,
+// no spills); the mirror fold (c + km*(...), evaluated back to front as the
+// recursion rounds) lives in scratch and is touched only by mirror lanes.
+// Same arithmetic per sample as render_kernel.
+__global__ __launch_bounds__(kWaveSize, RT_LV_MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
     const int lane = threadIdx.x & 63;
-    int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem + lane, ovf};
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x;
-    if (wid >= F.num_tiles) return;
+    if (wid >= F.num_tiles) return;  // wave-uniform
     const int tile = F.tile_order ? rtt::cload(F.tile_order + wid) : wid;
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
-    bool act[N];
-    rtt::RayCtx r[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        int px, ly, gy, s;
-        act[j] = rts::slot_pixel(F, tile, lane, px, ly, gy, s, j);
-        f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
-        if (act[j]) {
-            rts::primary_ray(F, px, gy, s, o, d);
-            cnt.primary++;
-        }
-        rtt::setup_ray(r[j], o, d);
-    }
-    rtp::PacketLane P[N];
+    float fold_c[kMaxBounces][3];
+    float fold_k[kMaxBounces][3];
+    int depth = 0;
+    f3 term = mk(0.0f, 0.0f, 0.0f);
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+    bool alive;
     {
-        const float zero[N] = {0.0f, 0.0f};
-        rtp::packet_trace_n<false, false, N>(S, r, act, zero, zero, P, wstack_mem, cnt);
+        int px, ly, gy, s;
+        alive = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
+        if (alive) {
+            rts::primary_ray(F, px, gy, s, o, d);
+            cnt.primary = 1;
+        }
     }
-    bool hit[N];
-    rts::Surface sf[N];
-    f3 col[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        hit[j] = act[j] && P[j].best_rank >= 0;
-        col[j] = mk(0.0f, 0.0f, 0.0f);
-        if (hit[j]) {
-            sf[j] = rts::surface(S, r[j].o, r[j].d, P[j].best_t, P[j].best_rank);
-            col[j] = rts::ambient(S, S.mats[sf[j].mat]);
+    for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
+        rtt::RayCtx r;
+        rtt::setup_ray(r, o, d);
+        rtp::PacketLane P;
+        rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt);
+        const bool hit = alive && P.best_rank >= 0;
+        if (alive && !hit) term = rtt::ld3(F.bg255);  // :310-311
+        rts::Surface sf;
+        f3 col = mk(0.0f, 0.0f, 0.0f);
+        int mat = 0;
+        if (hit) {
+            sf = rts::surface(S, o, d, P.best_t, P.best_rank);
+            mat = sf.mat;
+            col = rts::ambient(S, S.mats[mat]);
         } else {
-            sf[j].p = sf[j].n = sf[j].view = mk(0.0f, 0.0f, 1.0f);
-            sf[j].mat = 0;
+            sf.p = sf.n = sf.view = mk(0.0f, 0.0f, 1.0f);
+            sf.mat = 0;
         }
-    }
-    for (int l = 0; l < S.num_lights; ++l) {  // :327-356, wave-uniform
-        const DevLight Lt = S.lights[l];
-        rts::ShadowRay sr[N];
-        rtt::RayCtx rs[N];
-        float tl[N], d2[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-            sr[j] = rts::shadow_ray(sf[j], Lt);
-            if (hit[j]) cnt.shadow++;
-            rtt::setup_ray(rs[j], sr[j].o, sr[j].dir);
-            tl[j] = sqrtf(sr[j].d2) * 1.001f;
-            d2[j] = sr[j].d2;
+        for (int l = 0; l < S.num_lights; ++l) {  // :327-356, wave-uniform
+            const DevLight Lt = S.lights[l];
+            const rts::ShadowRay sr = rts::shadow_ray(sf, Lt);
+            if (hit) cnt.shadow++;
+            rtt::RayCtx rs;
+            rtt::setup_ray(rs, sr.o, sr.dir);
+            rtp::PacketLane Q;
+            rtp::packet_trace<true, false>(S, rs, hit, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+            if (hit && Q.best_rank != 1) col = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
         }
-        rtp::PacketLane Q[N];
-        rtp::packet_trace_n<true, false, N>(S, rs, hit, tl, d2, Q, wstack_mem, cnt);
-#pragma unroll
-        for (int j = 0; j < N; ++j)
-            if (hit[j] && Q[j].best_rank != 1) col[j] = col[j] + rts::light_term(S, sf[j], S.mats[sf[j].mat], Lt, sr[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        f3 term = mk(0.0f, 0.0f, 0.0f);
-        if (act[j]) {
-            if (!hit[j]) {
-                term = rtt::ld3(F.bg255);  // :310-311
+        bool mirror = false;
+        if (hit) {
+            const DevMaterial m = S.mats[mat];
+            mirror = m.ka_mirror.w != 0.0f && level < F.max_bounces;  // :358
+            if (mirror) {
+                fold_c[depth][0] = col.x; fold_c[depth][1] = col.y; fold_c[depth][2] = col.z;
+                fold_k[depth][0] = m.km.x; fold_k[depth][1] = m.km.y; fold_k[depth][2] = m.km.z;
+                rts::reflect(sf, o, d);
+                ++depth;
+                cnt.reflection++;
             } else {
-                const DevMaterial m = S.mats[sf[j].mat];
-                term = col[j];
-                if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363
-                    cnt.reflection++;
-                    f3 ro, rd;
-                    rts::reflect(sf[j], ro, rd);
-                    const f3 below = shade_levels<false>(S, F, ro, rd, 1, st, cnt);
-                    term = col[j] + mk(m.km.x, m.km.y, m.km.z) * below;
-                }
+                term = col;
             }
         }
-        const f3 sum = rts::sample_sum(term, lane, F.spp);
+        alive = mirror;
+    }
+    for (int k = depth - 1; k >= 0; --k)
+        term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
+    const f3 sum = rts::sample_sum(term, lane, F.spp);
+    {
         int tile2 = __builtin_amdgcn_readfirstlane(tile);
         asm volatile("" : "+s"(tile2));
         int px, ly, gy, s;
-        if (rts::slot_pixel(F, tile2, lane, px, ly, gy, s, j) && s == 0) {
+        if (rts::slot_pixel(F, tile2, lane, px, ly, gy, s) && s == 0) {
             f3 v = sum;
             if (F.spp > 1) v = v / (float)F.spp;
             rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
@@ -496,13 +480,23 @@ __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int ba
 
 namespace rtk {
 
+#ifndef RT_MK_LEVELS
+#define RT_MK_LEVELS 1
+#endif
+// all-packet levels pay off where a wave's tile is small on screen (its
+// mirror rays stay coherent): 16+ samples per pixel = at most 2x2 pixels
+#ifndef RT_MK_LEVELS_MIN_SPP
+#define RT_MK_LEVELS_MIN_SPP 16
+#endif
+
+
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
     const int blocks = (F.num_tiles + kMkWaves - 1) / kMkWaves;
     if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    else if (F.slots_per_lane == 2)
-        hipLaunchKernelGGL(render_pair_kernel, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S, F);
+    else if (RT_MK_LEVELS && S.bvh4 && F.spp >= RT_MK_LEVELS_MIN_SPP)
+        hipLaunchKernelGGL(render_levels_kernel, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S, F);
     else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     return hipGetLastError();
