@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
 }
 
 #ifndef RT_LV_MIN_WAVES
-#define RT_LV_MIN_WAVES 6
+#define RT_LV_MIN_WAVES 7
 #endif
 
 // Level-synchronous all-packet megakernel (the default non-counting path on
