@@ -56,6 +56,29 @@ def test_frame_vs_oracle(gpu_ctx, rt, orc, name, res, spp, mode):
     _check(img, ref, st, counts, f"{name}/{mode}")
 
 
+@pytest.mark.parametrize("name,res,spp", [("C3", (48, 27), 16), ("C2", (40, 24), 64), ("C5", (24, 14), 16)])
+def test_levels_kernel_vs_oracle(gpu_ctx, rt, orc, name, res, spp):
+    """>= 16 spp frames take the level-synchronous all-packet megakernel
+    (render_levels_kernel): whole frames against the oracle, mirror chains
+    and their shadow rays included."""
+    fr = rt.make(name).with_resolution(*res).with_(spp=spp)
+    img, st = _render(gpu_ctx, rt, fr)
+    ref, counts = orc.render(fr)
+    _check(img, ref, st, counts, f"{name}/levels/{spp}spp")
+
+
+def test_levels_kernel_bit_identical_to_other_paths(gpu_ctx, rt):
+    """The levels kernel, the level-synchronous packet kernel (per-lane deep
+    levels) and the wavefront path give the same bits and ray counts."""
+    fr = rt.make("C3").with_resolution(480, 270).with_(spp=16)
+    a, sa = _render(gpu_ctx, rt, fr, flags=0)
+    for flags in (2, 4):
+        b, sb = _render(gpu_ctx, rt, fr, flags=flags)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), flags
+        assert (sa.primary_rays, sa.shadow_rays, sa.reflection_rays) == (sb.primary_rays, sb.shadow_rays,
+                                                                         sb.reflection_rays), flags
+
+
 def test_modes_bit_identical_full_c3(gpu_ctx, rt):
     """Megakernel, wavefront and packet frames are bit-identical at full C3
     size, and so are their ray counts."""

@@ -18,6 +18,10 @@ hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const
 hipError_t launch_render_mega(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
                               hipStream_t stream);
 
+// Level-synchronous all-packet megakernel (trace_levels.hip), chosen by
+// launch_render_mega for >= 16 spp on a 4-wide BVH.
+hipError_t launch_render_levels(const rtd::SceneDev &S, const rtd::FrameDev &F, hipStream_t stream);
+
 // Packet megakernel: wave-synchronous levels, coherent rays traced one BVH
 // path per wave (packet.h).
 hipError_t launch_render_packet(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,

@@ -384,7 +384,7 @@ hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
     return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
 }
 
-constexpr int kLptPeriod = 4;  // frames between longest-first re-sorts
+constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 
 // Sums the sharded ray/test counters on the host (the stream must be idle).
 int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {

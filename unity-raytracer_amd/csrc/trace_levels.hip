@@ -1,0 +1,135 @@
+// trace_levels.hip — the level-synchronous all-packet megakernel (the
+// default non-counting path for >= 16 spp on a 4-wide BVH).  A file of its
+// own so it is compiled with the default GCN machine scheduler (trace.hip
+// uses the memory-clause strategy, which costs this kernel 4 % on C4).
+// RayTracingSetup.Shade (Assets/RayTracer/Demo-RayTracing/
+// RayTracingSetup.cs:304-366) per sample, exactly as render_kernel.
+#include <float.h>
+
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+#include "packet.h"
+#include "rt_device.h"
+#include "rt_math.h"
+#include "shade.h"
+#include "traverse.h"
+
+using namespace rtd;
+using rtm::f3;
+using rtm::mk;
+using rtt::Counts;
+
+namespace {
+
+#ifndef RT_LV_MIN_WAVES
+#define RT_LV_MIN_WAVES 7
+#endif
+
+// Level-synchronous all-packet megakernel (the default non-counting path on
+// a 4-wide BVH): one wave = one tile of 64 samples; the Whitted chain
+// advances level by level for the whole wave, and every level's rays — the
+// camera rays, the mirror rays of the lanes still bouncing, and each level's
+// shadow rays — are traced as wave packets (packet.h).  Without a per-lane
+// traversal the kernel needs no LDS lane stack and ~80 VGPRs (6 waves/SIMD,
+// no spills); the mirror fold (c + km*(...), evaluated back to front as the
+// recursion rounds) lives in scratch and is touched only by mirror lanes.
+// Same arithmetic per sample as render_kernel.
+__global__ __launch_bounds__(kWaveSize, RT_LV_MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
+    __shared__ int wstack_mem[rtp::kWaveStack];
+    const int lane = threadIdx.x & 63;
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    const int wid = blockIdx.x;
+    if (wid >= F.num_tiles) return;  // wave-uniform
+    const int tile = F.tile_order ? rtt::cload(F.tile_order + wid) : wid;
+    const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
+    float fold_c[kMaxBounces][3];
+    float fold_k[kMaxBounces][3];
+    int depth = 0;
+    f3 term = mk(0.0f, 0.0f, 0.0f);
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+    bool alive;
+    {
+        int px, ly, gy, s;
+        alive = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
+        if (alive) {
+            rts::primary_ray(F, px, gy, s, o, d);
+            cnt.primary = 1;
+        }
+    }
+    for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
+        rtt::RayCtx r;
+        rtt::setup_ray(r, o, d);
+        rtp::PacketLane P;
+        rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt);
+        const bool hit = alive && P.best_rank >= 0;
+        if (alive && !hit) term = rtt::ld3(F.bg255);  // :310-311
+        rts::Surface sf;
+        f3 col = mk(0.0f, 0.0f, 0.0f);
+        int mat = 0;
+        if (hit) {
+            sf = rts::surface(S, o, d, P.best_t, P.best_rank);
+            mat = sf.mat;
+            col = rts::ambient(S, S.mats[mat]);
+        } else {
+            sf.p = sf.n = sf.view = mk(0.0f, 0.0f, 1.0f);
+            sf.mat = 0;
+        }
+        for (int l = 0; l < S.num_lights; ++l) {  // :327-356, wave-uniform
+            const DevLight Lt = S.lights[l];
+            const rts::ShadowRay sr = rts::shadow_ray(sf, Lt);
+            if (hit) cnt.shadow++;
+            rtt::RayCtx rs;
+            rtt::setup_ray(rs, sr.o, sr.dir);
+            rtp::PacketLane Q;
+            rtp::packet_trace<true, false>(S, rs, hit, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+            if (hit && Q.best_rank != 1) col = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
+        }
+        bool mirror = false;
+        if (hit) {
+            const DevMaterial m = S.mats[mat];
+            mirror = m.ka_mirror.w != 0.0f && level < F.max_bounces;  // :358
+            if (mirror) {
+                fold_c[depth][0] = col.x; fold_c[depth][1] = col.y; fold_c[depth][2] = col.z;
+                fold_k[depth][0] = m.km.x; fold_k[depth][1] = m.km.y; fold_k[depth][2] = m.km.z;
+                rts::reflect(sf, o, d);
+                ++depth;
+                cnt.reflection++;
+            } else {
+                term = col;
+            }
+        }
+        alive = mirror;
+    }
+    for (int k = depth - 1; k >= 0; --k)
+        term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
+    const f3 sum = rts::sample_sum(term, lane, F.spp);
+    {
+        int tile2 = __builtin_amdgcn_readfirstlane(tile);
+        asm volatile("" : "+s"(tile2));
+        int px, ly, gy, s;
+        if (rts::slot_pixel(F, tile2, lane, px, ly, gy, s) && s == 0) {
+            f3 v = sum;
+            if (F.spp > 1) v = v / (float)F.spp;
+            rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+        }
+    }
+    if (F.tile_cost && lane == 0) {
+        const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
+        const unsigned e = c ? 31u - __clz(c) : 0u;
+        F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
+    }
+    rtt::flush_counts<false>(cnt, F.counters);
+}
+
+}  // namespace
+
+namespace rtk {
+
+hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F, hipStream_t stream) {
+    if (F.num_tiles <= 0) return hipSuccess;
+    hipLaunchKernelGGL(render_levels_kernel, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S, F);
+    return hipGetLastError();
+}
+
+}  // namespace rtk
