@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams consecutive frames alternate on (frames in flight; 1 = one frame at a time)")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
+    ap.add_argument("--sim-bands", type=int, default=0,
+                    help="experiment (one GPU, no gather): render only row band 0 of N, i.e. one rank's share "
+                         "of an N-GPU frame")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the distributed path (process group, async gather, reassembly) even at one rank")
     ap.add_argument("--dist-backend", default="nccl",
@@ -135,8 +138,8 @@ def main():
     ctx.set_scene(fr.scene)
     rx, ry = fr.plane.ResolutionX, fr.plane.ResolutionY
     R = 8
-    band_count = world
-    local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if dist_on else ry
+    band_count = world if not args.sim_bands else args.sim_bands
+    local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if (dist_on or args.sim_bands) else ry
     # Frames rotate over nbuf output buffers and `--streams` HIP streams (more
     # than one stream = frames in flight, off by default).  N > 1: each
     # buffer's shard is gathered to rank 0 over RCCL asynchronously (the NCCL
