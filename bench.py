@@ -99,8 +99,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: check the assembled frame against 1 rank")
     ap.add_argument("--mode", choices=["megakernel", "wavefront", "packet"], default="megakernel")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="HIP streams consecutive frames alternate on (frames in flight; 1 = one frame at a time)")
+    ap.add_argument("--streams", type=int, default=3,
+                    help="HIP streams consecutive frames alternate on: frames in flight, so one frame's slowest "
+                         "tiles overlap the next frame's bulk (1 = one frame at a time)")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--sim-bands", type=int, default=0,
                     help="experiment (one GPU, no gather): render only row band 0 of N, i.e. one rank's share "
@@ -124,6 +125,8 @@ def main():
     torch.cuda.set_device(device)
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:  # --force-dist outside a launcher
+            os.environ.setdefault("MASTER_PORT", "29531")
         if gloo:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:

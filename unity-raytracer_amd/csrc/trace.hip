@@ -227,11 +227,20 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
             vi = max(vi, (unsigned long long)__shfl_xor((long long)vi, off));
         }
         if (lane == 0) {
+#ifdef RT_SEG_MAX
+            // the slowest wave instead of sums (slot 0 only: the host sums slots)
+            unsigned long long *ctr = F.counters;
+            atomicMax(ctr + 3, (vi & 0xffffffffull) + (vi >> 32));  // packet node + leaf visits
+            atomicMax(ctr + 4, pr);
+            atomicMax(ctr + 5, sh);
+            atomicMax(ctr + 6, ts1 - ts0);
+#else
             unsigned long long *ctr = F.counters + (size_t)(blockIdx.x % kCounterSlots) * kCounterWords;
             atomicAdd(ctr + 3, vi);  // packet visits: internal | leaves << 32 (setup clock su unused)
             atomicAdd(ctr + 4, pr);
             atomicAdd(ctr + 5, sh);
             atomicAdd(ctr + 6, ts1 - ts0);
+#endif
         }
     }
 #endif
