@@ -289,3 +289,18 @@ def test_longest_first_order_is_invisible(gpu_ctx, rt):
         c, _ = gpu_ctx.render(fr2.camera, fr2.plane, rt.frame_params(fr2))
     d, _ = gpu_ctx.render(fr2.camera, fr2.plane, rt.frame_params(fr2, flags=rt.abi.RT_FLAG_ROW_ORDER))
     assert np.array_equal(c.view(np.uint32), d.view(np.uint32))
+
+
+def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
+    """Small frames (<= 24,000 tiles) run their slowest tiles, as measured by
+    the previous re-sort, as four quarter-waves: same bits and same ray counts
+    as row-major whole-tile frames, for a whole frame and for a row shard."""
+    fr = rt.make("C3").with_resolution(640, 360)
+    gpu_ctx.set_scene(fr.scene)
+    for kw in ({}, dict(band_index=1, band_count=3, band_rows=8)):
+        row, sr = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
+        for _ in range(3):  # the first frame measures and sorts; later ones split
+            img, st = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
+            assert np.array_equal(img.view(np.uint32), row.view(np.uint32)), kw
+            assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == (sr.primary_rays, sr.shadow_rays,
+                                                                             sr.reflection_rays), kw

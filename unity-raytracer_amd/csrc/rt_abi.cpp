@@ -384,6 +384,16 @@ hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
     return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
 }
 
+#ifndef RT_SPLIT_DIV
+#define RT_SPLIT_DIV 256
+#endif
+// Quarter-wave splitting of a frame's slowest tiles trades extra work (each
+// quarter re-walks the BVH top) for a shorter critical path; it pays only
+// when the frame (shard) is small enough for its slowest wave to set its
+// time: measured with 3 frames in flight, a 1/8 C3 shard (16,200 tiles)
+// +18 %, a 1/4 shard (32,400) -7 %, a whole frame (129,600) -7 %.
+constexpr int kSplitDiv = RT_SPLIT_DIV;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
+constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this many tiles
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 
 // Sums the sharded ray/test counters on the host (the stream must be idle).
@@ -500,6 +510,12 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         lpt_sort = !ls->valid || ls->frames % kLptPeriod == 0;
         F.tile_cost = lpt_sort ? (unsigned *)ls->cost.p : nullptr;
         ++ls->frames;
+        // the most expensive tiles of the last measurement are split into
+        // quarter-waves (a frame's time is bounded below by its slowest
+        // wave); render_kernel only: 16 lanes must hold whole pixels
+        const bool levels = ctx->S.bvh4 && F.spp >= 16;
+        if (F.tile_order && !count && !levels && kSplitDiv > 0 && 16 % F.spp == 0 && F.num_tiles <= kSplitMaxTiles)
+            F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
     }
     if (packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));

@@ -171,11 +171,14 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 
 // One tile (a wave) of the megakernel: trace every sample, sum a pixel's
 // samples in row-major sample order ((s0 + s1) + s2) + ..., store.
+// quarter >= 0: this wave takes only lanes [16 * quarter, 16 * quarter + 16)
+// of the tile (one of the four waves an expensive tile is split into).
 template <bool COUNT>
 __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
-                                            int *wstack, int tile, int lane, Counts &cnt, SegClock &sg) {
+                                            int *wstack, int tile, int quarter, int lane, Counts &cnt,
+                                            SegClock &sg) {
     int px, ly, gy, s;
-    const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
+    const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s) && (quarter < 0 || (lane >> 4) == quarter);
     f3 color = mk(0.0f, 0.0f, 0.0f);
     if (active) {
         f3 o, d;
@@ -188,7 +191,7 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     // rather than kept live across the trace, where it would be spilled
     int tile2 = __builtin_amdgcn_readfirstlane(tile);
     asm volatile("" : "+s"(tile2));
-    const bool active2 = rts::slot_pixel(F, tile2, lane, px, ly, gy, s);
+    const bool active2 = rts::slot_pixel(F, tile2, lane, px, ly, gy, s) && (quarter < 0 || (lane >> 4) == quarter);
     if (active2 && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
@@ -208,13 +211,22 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     int *const wstack = wstack_mem + (kPackets ? wave * rtp::kWaveStack : 0);
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x * kMkWaves + wave;
-    if (wid >= F.num_tiles) return;  // wave-uniform
-    // dispatch order: the previous frame's most expensive tiles first (F.tile_order)
-    const int tile = F.tile_order ? rtt::cload(F.tile_order + wid) : wid;  // scalar load: tile math stays SALU
+    if (wid >= F.num_tiles + 3 * F.split_tiles) return;  // wave-uniform
+    // dispatch order: the previous frame's most expensive tiles first
+    // (F.tile_order); the first split_tiles of them as four quarter-waves
+    // each (16 lanes: a smaller, more coherent packet, a shorter wave)
+    int tile, quarter = -1;
+    if (wid < 4 * F.split_tiles) {
+        tile = rtt::cload(F.tile_order + (wid >> 2));  // scalar load: tile math stays SALU
+        quarter = wid & 3;
+    } else {
+        const int w2 = wid - 3 * F.split_tiles;
+        tile = F.tile_order ? rtt::cload(F.tile_order + w2) : w2;
+    }
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    render_tile<COUNT>(S, F, st, wstack, tile, lane, cnt, sg);
+    render_tile<COUNT>(S, F, st, wstack, tile, quarter, lane, cnt, sg);
 #ifdef RT_SEG_PROFILE
     if (!COUNT) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -244,9 +256,12 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
         }
     }
 #endif
-    if (F.tile_cost && lane == 0) {
-        // log-scale cost key (4 mantissa bits, < 512): one cheap sort pass set
-        const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
+    if (F.tile_cost && lane == 0 && quarter <= 0) {
+        // log-scale cost key (4 mantissa bits, < 512): one cheap sort pass
+        // set; a split tile is charged four times its first quarter
+        unsigned long long c64 = __builtin_amdgcn_s_memtime() - t0;
+        if (quarter == 0) c64 *= 4;
+        const unsigned c = (unsigned)min(c64, 0xffffffffull);
         const unsigned e = c ? 31u - __clz(c) : 0u;
         F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
     }
@@ -401,7 +416,7 @@ namespace rtk {
 
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
-    const int blocks = (F.num_tiles + kMkWaves - 1) / kMkWaves;
+    const int blocks = (F.num_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
     if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (RT_MK_LEVELS && S.bvh4 && F.spp >= RT_MK_LEVELS_MIN_SPP)
