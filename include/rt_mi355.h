@@ -148,6 +148,10 @@ typedef struct rt_render_params {
  * the shard gather and the D2H copy shrink 4x / 2x. */
 #define RT_FLAG_OUT_RGBA8   8   /* Color32: round-half-even(clamp01(c) * 255), alpha 255; 4 B */
 #define RT_FLAG_OUT_RGBA16F 16  /* IEEE half RGBA (round to nearest even), alpha 1, unclamped; 8 B */
+/* Float RGB without the constant alpha (Rgb.Color's a is always 1): the
+ * Color values bit for bit in 12 B — a shard transport format that cuts the
+ * framebuffer gather by a quarter. */
+#define RT_FLAG_OUT_RGB32F  128
 /* rt_render_device only: enqueue the frame on the context's stream and return
  * without waiting (a frame loop that keeps the GPU fed; switching the stream
  * with rt_set_stream between frames lets consecutive frames overlap).  The
@@ -281,7 +285,7 @@ int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
  * since the first of them was enqueued. */
 int rt_finish(rt_ctx *ctx, rt_stats *stats);
 
-/* Bytes per output pixel for rt_render_params.flags: 16, 8 or 4. */
+/* Bytes per output pixel for rt_render_params.flags: 16, 12, 8 or 4. */
 int32_t rt_pixel_bytes(int32_t flags);
 
 /* Same as rt_render but the output stays in HBM: d_out_rgba is a DEVICE

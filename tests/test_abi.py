@@ -85,3 +85,16 @@ def test_create_without_gpu_fails_loudly(rt):
     with pytest.raises(rt.RtError) as e:
         rt.Context()
     assert e.value.status in (rt.abi.RT_E_NO_DEVICE, rt.abi.RT_E_HIP)
+
+
+def test_pixel_bytes_per_format(rt):
+    """rt_pixel_bytes (host-only, no GPU needed): float RGBA 16, RGB32F 12,
+    RGBA16F 8, RGBA8 4; and the Python flag constants equal the header's."""
+    lib = rt.load_library()
+    a = rt.abi
+    assert [lib.rt_pixel_bytes(f) for f in (0, a.RT_FLAG_OUT_RGB32F, a.RT_FLAG_OUT_RGBA16F, a.RT_FLAG_OUT_RGBA8)] == \
+        [16, 12, 8, 4]
+    import re
+    hdr = open(os.path.join(ROOT, "include", "rt_mi355.h")).read()
+    for name, val in re.findall(r"#define (RT_FLAG_\w+)\s+(\d+)", hdr):
+        assert getattr(a, name) == int(val), name

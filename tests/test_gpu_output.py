@@ -10,7 +10,7 @@ import np_oracle as npo
 
 pytestmark = pytest.mark.gpu
 
-F8, F16 = 8, 16
+F8, F16, F12 = 8, 16, 128
 
 
 @pytest.mark.parametrize("mode", [0, 2, 4])
@@ -28,7 +28,7 @@ def test_encoded_frames_equal_encoded_float_frame(gpu_ctx, rt, mode):
     assert (sf.primary_rays, sf.shadow_rays) == (sb.primary_rays, sb.shadow_rays) == (sh.primary_rays, sh.shadow_rays)
 
 
-@pytest.mark.parametrize("flags,pb", [(F8, 4), (F16, 8), (0, 16)])
+@pytest.mark.parametrize("flags,pb", [(F8, 4), (F16, 8), (F12, 12), (0, 16)])
 def test_encoded_bands_reassemble(gpu_ctx, rt, flags, pb):
     import torch
     fr = rt.make("C2").with_resolution(150, 77)
@@ -48,6 +48,20 @@ def test_encoded_bands_reassemble(gpu_ctx, rt, flags, pb):
     assert np.array_equal(got.view(np.uint8), full.view(np.uint8))
 
 
+@pytest.mark.parametrize("mode", [0, 2, 4])
+def test_rgb32f_is_the_float_frame_without_alpha(gpu_ctx, rt, mode):
+    """RT_FLAG_OUT_RGB32F (the shard transport format): the Color values bit
+    for bit, 12 B per pixel, for every render path and a >= 16 spp frame."""
+    for fr in (rt.make("C2").with_resolution(120, 67), rt.make("C3").with_resolution(64, 36).with_(spp=16)):
+        gpu_ctx.set_scene(fr.scene)
+        f, sf = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=mode))
+        c, sc = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=mode | F12))
+        assert c.shape == f.shape[:2] + (3,) and c.dtype == np.float32
+        assert np.array_equal(c.view(np.uint32), np.ascontiguousarray(f[..., :3]).view(np.uint32))
+        assert (sf.primary_rays, sf.shadow_rays, sf.reflection_rays) == (sc.primary_rays, sc.shadow_rays,
+                                                                         sc.reflection_rays)
+
+
 def test_rgba8_ppm_writer(gpu_ctx, rt, tmp_path):
     fr = rt.make("demo")
     gpu_ctx.set_scene(fr.scene)
@@ -63,4 +77,7 @@ def test_exclusive_formats(gpu_ctx, rt):
     gpu_ctx.set_scene(fr.scene)
     with pytest.raises(rt.RtError) as e:
         gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=F8 | F16))
+    assert e.value.status == rt.abi.RT_E_INVALID
+    with pytest.raises(rt.RtError) as e:
+        gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=F12 | F16))
     assert e.value.status == rt.abi.RT_E_INVALID

@@ -28,6 +28,7 @@ RT_FLAG_WAVEFRONT = 2
 RT_FLAG_PACKET = 4
 RT_FLAG_OUT_RGBA8 = 8
 RT_FLAG_OUT_RGBA16F = 16
+RT_FLAG_OUT_RGB32F = 128
 RT_FLAG_ASYNC = 32
 RT_FLAG_ROW_ORDER = 64
 RT_BUILD_SAH_HOST = 0

@@ -302,9 +302,11 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.tiles_x = (F.res_x + tw - 1) / tw;
     const int tiles_y = (F.local_rows + th - 1) / th;
     F.num_tiles = F.res_x > 0 ? F.tiles_x * tiles_y : 0;
-    const bool f8 = (prm->flags & RT_FLAG_OUT_RGBA8) != 0, f16 = (prm->flags & RT_FLAG_OUT_RGBA16F) != 0;
-    if (f8 && f16) return fail(ctx, RT_E_INVALID, "RT_FLAG_OUT_RGBA8 and RT_FLAG_OUT_RGBA16F are exclusive");
-    F.out_format = f8 ? rtd::kOutRGBA8 : (f16 ? rtd::kOutRGBA16F : rtd::kOutFloat4);
+    const bool f8 = (prm->flags & RT_FLAG_OUT_RGBA8) != 0, f16 = (prm->flags & RT_FLAG_OUT_RGBA16F) != 0,
+               f12 = (prm->flags & RT_FLAG_OUT_RGB32F) != 0;
+    if ((int)f8 + (int)f16 + (int)f12 > 1)
+        return fail(ctx, RT_E_INVALID, "RT_FLAG_OUT_RGBA8, RT_FLAG_OUT_RGBA16F and RT_FLAG_OUT_RGB32F are exclusive");
+    F.out_format = f8 ? rtd::kOutRGBA8 : (f16 ? rtd::kOutRGBA16F : (f12 ? rtd::kOutRGB32F : rtd::kOutFloat4));
     out_bytes = (size_t)F.local_rows * F.res_x * rt_pixel_bytes(prm->flags);
     return RT_OK;
 }
@@ -1240,14 +1242,14 @@ int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x
 }
 
 int32_t rt_pixel_bytes(int32_t flags) {
-    return (flags & RT_FLAG_OUT_RGBA8) ? 4 : ((flags & RT_FLAG_OUT_RGBA16F) ? 8 : 16);
+    return (flags & RT_FLAG_OUT_RGBA8) ? 4 : ((flags & RT_FLAG_OUT_RGBA16F) ? 8 : ((flags & RT_FLAG_OUT_RGB32F) ? 12 : 16));
 }
 
 int rt_assemble_bands_ex(rt_ctx *ctx, const void *d_gathered, int32_t resolution_x, int32_t resolution_y,
                          int32_t band_count, int32_t band_rows, int32_t pixel_bytes, void *d_image) {
     if (!ctx) return RT_E_INVALID;
     if (!d_gathered || !d_image || resolution_x < 0 || resolution_y < 0 || band_count < 1 ||
-        (pixel_bytes != 4 && pixel_bytes != 8 && pixel_bytes != 16))
+        (pixel_bytes != 4 && pixel_bytes != 8 && pixel_bytes != 12 && pixel_bytes != 16))
         return fail(ctx, RT_E_INVALID, "bad rt_assemble_bands arguments");
     if (band_rows <= 0) band_rows = 8;
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));

@@ -55,6 +55,7 @@ constexpr int kLeafSphere = 1;
 constexpr int kOutFloat4 = 0;   // Color, 16 B (the reference's Color[])
 constexpr int kOutRGBA8 = 1;    // Color32, 4 B
 constexpr int kOutRGBA16F = 2;  // half RGBA, 8 B
+constexpr int kOutRGB32F = 3;   // float RGB (alpha 1 implied), 12 B
 
 struct alignas(16) BvhNode {
     float4 a;  // child0 lo.x, hi.x, lo.y, hi.y
@@ -170,7 +171,7 @@ struct FrameDev {
     void *out;               // local_rows x res_x pixels in out_format
     const int *tile_order;   // megakernel dispatch order (null: row-major)
     unsigned *tile_cost;     // per-tile cost of this frame (shader clock), null: not recorded
-    int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F
+    int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F / kOutRGB32F
     int split_tiles;         // render_kernel: the first split_tiles of tile_order run as 4 quarter-waves each
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
 };

@@ -177,6 +177,11 @@ __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, 
     const float r = v.x / 255.0f, g = v.y / 255.0f, b = v.z / 255.0f;
     if (F.out_format == rtd::kOutRGBA8) {
         ((unsigned *)F.out)[idx] = encode8(r) | (encode8(g) << 8) | (encode8(b) << 16) | (255u << 24);
+    } else if (F.out_format == rtd::kOutRGB32F) {
+        float *q = (float *)F.out + idx * 3;
+        q[0] = r;
+        q[1] = g;
+        q[2] = b;
     } else if (F.out_format == rtd::kOutRGBA16F) {
         ((uint2 *)F.out)[idx] = make_uint2(half_bits(r) | (half_bits(g) << 16), half_bits(b) | (0x3C00u << 16));
     } else {

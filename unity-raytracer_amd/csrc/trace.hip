@@ -199,7 +199,9 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     }
 }
 
-template <bool COUNT>
+// SPLIT: the variant launched when F.split_tiles > 0 (a separate instance, so
+// the common kernel's code and register allocation stay as they are).
+template <bool COUNT, bool SPLIT = false>
 __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
     constexpr bool kPackets = RT_MK_PACKET_SHADOW || RT_MK_PACKET_PRIMARY;
@@ -211,16 +213,18 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     int *const wstack = wstack_mem + (kPackets ? wave * rtp::kWaveStack : 0);
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x * kMkWaves + wave;
-    if (wid >= F.num_tiles + 3 * F.split_tiles) return;  // wave-uniform
+    const int split = SPLIT ? F.split_tiles : 0;
+    if (wid >= F.num_tiles + 3 * split) return;  // wave-uniform
     // dispatch order: the previous frame's most expensive tiles first
-    // (F.tile_order); the first split_tiles of them as four quarter-waves
-    // each (16 lanes: a smaller, more coherent packet, a shorter wave)
+    // (F.tile_order); SPLIT: the first split_tiles of them as four
+    // quarter-waves each (16 lanes: a smaller, more coherent packet, a
+    // shorter wave)
     int tile, quarter = -1;
-    if (wid < 4 * F.split_tiles) {
+    if (SPLIT && wid < 4 * split) {
         tile = rtt::cload(F.tile_order + (wid >> 2));  // scalar load: tile math stays SALU
         quarter = wid & 3;
     } else {
-        const int w2 = wid - 3 * F.split_tiles;
+        const int w2 = wid - 3 * split;
         tile = F.tile_order ? rtt::cload(F.tile_order + w2) : w2;
     }
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -387,6 +391,10 @@ __global__ __launch_bounds__(kBlockThreads) void intersect_kernel(SceneDev S, co
     out[i] = make_int4(br, __float_as_int(bt), 0, 0);
 }
 
+struct Px12 {  // float RGB pixel (RT_FLAG_OUT_RGB32F)
+    float v[3];
+};
+
 template <typename Px>
 __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int band_count, int band_rows,
                                 int local_rows, Px *image) {
@@ -419,6 +427,8 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
     const int blocks = (F.num_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
     if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+    else if (F.split_tiles > 0)
+        hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (RT_MK_LEVELS && S.bvh4 && F.spp >= RT_MK_LEVELS_MIN_SPP)
         return launch_render_levels(S, F, stream);
     else
@@ -474,6 +484,9 @@ hipError_t launch_assemble(const void *gathered, int res_x, int res_y, int band_
     if (pixel_bytes == 16)
         hipLaunchKernelGGL(assemble_kernel<float4>, dim3(blocks), dim3(threads), 0, stream, (const float4 *)gathered,
                            res_x, res_y, band_count, band_rows, local_rows, (float4 *)image);
+    else if (pixel_bytes == 12)
+        hipLaunchKernelGGL(assemble_kernel<Px12>, dim3(blocks), dim3(threads), 0, stream, (const Px12 *)gathered,
+                           res_x, res_y, band_count, band_rows, local_rows, (Px12 *)image);
     else if (pixel_bytes == 8)
         hipLaunchKernelGGL(assemble_kernel<uint2>, dim3(blocks), dim3(threads), 0, stream, (const uint2 *)gathered,
                            res_x, res_y, band_count, band_rows, local_rows, (uint2 *)image);

@@ -30,6 +30,11 @@ def plane_struct(p: ImagePlane) -> abi.rt_image_plane:
                               float(p.HalfHorizontalLength), float(p.HalfVerticalLength))
 
 
+def channels(flags: int) -> int:
+    """Channels per output pixel: 3 for RT_FLAG_OUT_RGB32F, else 4."""
+    return 3 if flags & abi.RT_FLAG_OUT_RGB32F else 4
+
+
 def pixel_dtype(flags: int):
     """numpy dtype of one output channel for rt_render_params.flags."""
     if flags & abi.RT_FLAG_OUT_RGBA8:
@@ -133,9 +138,10 @@ class Context:
             rows = self.lib.rt_band_rows_local(plane.ResolutionY, params.band_index,
                                                params.band_count, params.band_rows)
         dtype = pixel_dtype(params.flags)
+        ch = channels(params.flags)
         if out is None:
-            out = np.empty((rows, plane.ResolutionX, 4), dtype)
-        assert out.dtype == dtype and out.flags.c_contiguous and out.size >= rows * plane.ResolutionX * 4
+            out = np.empty((rows, plane.ResolutionX, ch), dtype)
+        assert out.dtype == dtype and out.flags.c_contiguous and out.size >= rows * plane.ResolutionX * ch
         stats = abi.rt_stats()
         cam, pl = camera_struct(camera), plane_struct(plane)
         self._check(self.lib.rt_render(self.h, C.byref(cam), C.byref(pl), C.byref(params),
