@@ -261,6 +261,19 @@ def main():
         ctx.render_device(fr.camera, fr.plane, aparams, out.data_ptr(), nbytes)
     kernel_ms = ctx.finish().kernel_ms
 
+    # end-to-end rt_render (synchronous, host Color[] output: includes the D2H
+    # copy over PCIe), N = 1 only; reported beside `value`, never as it
+    e2e_ms = None
+    if not dist_on and not args.sim_bands and rank == 0:
+        host = np.empty((ry, rx, 4), dtype=np.float32)
+        ctx.set_stream(stream.cuda_stream)
+        ts = []
+        for _ in range(6):
+            t1 = time.perf_counter()
+            ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=mode_flags), out=host)
+            ts.append(time.perf_counter() - t1)
+        e2e_ms = float(np.median(ts[1:])) * 1e3
+
     if dist_on and args.verify:
         # the assembled frame must be bit-identical to a single-rank frame
         full = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda")
@@ -314,6 +327,9 @@ def main():
                 "rays_per_frame": rays // args.steps,
                 "frames_in_flight": nstreams,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
+                # primary samples (W*H*spp of the frame, or of this band) per second
+                "msamples_per_s": rx * (local_rows if args.sim_bands else ry) * fr.spp * args.steps / elapsed / 1e6,
+                "end_to_end_ms_per_frame": e2e_ms,
             },
             "roofline": {
                 "bound": "hbm",
