@@ -1,0 +1,40 @@
+"""Experiment check: a library variant's split frames equal row-major
+whole-tile frames bit for bit (C3 at 640x360 and 1/8 shards of 1080p).
+
+    python tools/split_check.py --lib s16_1024"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import _rt_pkg  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", default="")
+    a = ap.parse_args()
+    rt = _rt_pkg.load()
+    lib = os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", a.lib, "librt_mi355.so") if a.lib else None
+    ctx = rt.Context(lib_path=lib)
+    ok = True
+    for fr, kw in ((rt.make("C3").with_resolution(640, 360), {}),
+                   (rt.make("C3"), dict(band_index=3, band_count=8, band_rows=8))):
+        ctx.set_scene(fr.scene)
+        row, sr = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
+        for _ in range(3):
+            img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
+            same = np.array_equal(img.view(np.uint32), row.view(np.uint32)) and \
+                (st.primary_rays, st.shadow_rays, st.reflection_rays) == \
+                (sr.primary_rays, sr.shadow_rays, sr.reflection_rays)
+            ok &= bool(same)
+    print({"lib": a.lib or "default", "split_frames_identical": ok}, flush=True)
+    ctx.close()
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()

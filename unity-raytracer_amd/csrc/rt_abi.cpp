@@ -393,7 +393,14 @@ hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
 // quarter re-walks the BVH top) for a shorter critical path; it pays only
 // when the frame (shard) is small enough for its slowest wave to set its
 // time: measured with 3 frames in flight, a 1/8 C3 shard (16,200 tiles)
-// +18 %, a 1/4 shard (32,400) -7 %, a whole frame (129,600) -7 %.
+// +18 %, a 1/4 shard (32,400) -7 %, a whole frame (129,600) -7 %.  The very
+// slowest of them (1/2048 of the tiles) go further, to sixteen waves of one
+// pixel each: a 1/8 shard's single frame -14 % more, throughput with frames
+// in flight +-1 % (1/512 or more: -5..-15 %).
+#ifndef RT_SPLIT16_DIV
+#define RT_SPLIT16_DIV 2048
+#endif
+constexpr int kSplit16Div = RT_SPLIT16_DIV;  // of those, 1/kSplit16Div of the tiles as sixteenth-waves; 0: off
 constexpr int kSplitDiv = RT_SPLIT_DIV;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
 constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this many tiles
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
@@ -516,8 +523,14 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         // quarter-waves (a frame's time is bounded below by its slowest
         // wave); render_kernel only: 16 lanes must hold whole pixels
         const bool levels = ctx->S.bvh4 && F.spp >= 16;
-        if (F.tile_order && !count && !levels && kSplitDiv > 0 && 16 % F.spp == 0 && F.num_tiles <= kSplitMaxTiles)
+        if (F.tile_order && !count && !levels && kSplitDiv > 0 && 16 % F.spp == 0 && F.num_tiles <= kSplitMaxTiles) {
             F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
+            // sixteenth-waves (4 lanes) must hold whole pixels too
+            if (kSplit16Div > 0 && 4 % F.spp == 0) {
+                F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / kSplit16Div));
+                F.split_tiles -= F.split16_tiles;
+            }
+        }
     }
     if (packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));

@@ -172,7 +172,8 @@ struct FrameDev {
     const int *tile_order;   // megakernel dispatch order (null: row-major)
     unsigned *tile_cost;     // per-tile cost of this frame (shader clock), null: not recorded
     int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F / kOutRGB32F
-    int split_tiles;         // render_kernel: the first split_tiles of tile_order run as 4 quarter-waves each
+    int split16_tiles;       // render_kernel: the first split16_tiles of tile_order run as 16 sixteenth-waves each,
+    int split_tiles;         // ... the next split_tiles as 4 quarter-waves each
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
 };
 

@@ -171,14 +171,15 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 
 // One tile (a wave) of the megakernel: trace every sample, sum a pixel's
 // samples in row-major sample order ((s0 + s1) + s2) + ..., store.
-// quarter >= 0: this wave takes only lanes [16 * quarter, 16 * quarter + 16)
-// of the tile (one of the four waves an expensive tile is split into).
+// part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
+// one of the four (pshift 4: 16 lanes) or sixteen (pshift 2: 4 lanes) waves
+// an expensive tile is split into.
 template <bool COUNT>
 __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
-                                            int *wstack, int tile, int quarter, int lane, Counts &cnt,
+                                            int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
                                             SegClock &sg) {
     int px, ly, gy, s;
-    const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s) && (quarter < 0 || (lane >> 4) == quarter);
+    const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
     f3 color = mk(0.0f, 0.0f, 0.0f);
     if (active) {
         f3 o, d;
@@ -191,7 +192,7 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     // rather than kept live across the trace, where it would be spilled
     int tile2 = __builtin_amdgcn_readfirstlane(tile);
     asm volatile("" : "+s"(tile2));
-    const bool active2 = rts::slot_pixel(F, tile2, lane, px, ly, gy, s) && (quarter < 0 || (lane >> 4) == quarter);
+    const bool active2 = rts::slot_pixel(F, tile2, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
     if (active2 && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
@@ -199,7 +200,7 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     }
 }
 
-// SPLIT: the variant launched when F.split_tiles > 0 (a separate instance, so
+// SPLIT: the variant launched when a frame splits tiles (a separate instance, so
 // the common kernel's code and register allocation stay as they are).
 template <bool COUNT, bool SPLIT = false>
 __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
@@ -213,24 +214,31 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     int *const wstack = wstack_mem + (kPackets ? wave * rtp::kWaveStack : 0);
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x * kMkWaves + wave;
+    const int split16 = SPLIT ? F.split16_tiles : 0;
     const int split = SPLIT ? F.split_tiles : 0;
-    if (wid >= F.num_tiles + 3 * split) return;  // wave-uniform
+    if (wid >= F.num_tiles + 15 * split16 + 3 * split) return;  // wave-uniform
     // dispatch order: the previous frame's most expensive tiles first
-    // (F.tile_order); SPLIT: the first split_tiles of them as four
+    // (F.tile_order); SPLIT: the first split16_tiles of them as sixteen
+    // waves of one pixel's 4 samples each, the next split_tiles as four
     // quarter-waves each (16 lanes: a smaller, more coherent packet, a
     // shorter wave)
-    int tile, quarter = -1;
-    if (SPLIT && wid < 4 * split) {
-        tile = rtt::cload(F.tile_order + (wid >> 2));  // scalar load: tile math stays SALU
-        quarter = wid & 3;
+    int tile, part = -1, pshift = 4;
+    if (SPLIT && wid < 16 * split16) {
+        tile = rtt::cload(F.tile_order + (wid >> 4));  // scalar load: tile math stays SALU
+        part = wid & 15;
+        pshift = 2;
+    } else if (SPLIT && wid < 16 * split16 + 4 * split) {
+        const int w1 = wid - 16 * split16;
+        tile = rtt::cload(F.tile_order + split16 + (w1 >> 2));
+        part = w1 & 3;
     } else {
-        const int w2 = wid - 3 * split;
+        const int w2 = wid - 15 * split16 - 3 * split;
         tile = F.tile_order ? rtt::cload(F.tile_order + w2) : w2;
     }
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    render_tile<COUNT>(S, F, st, wstack, tile, quarter, lane, cnt, sg);
+    render_tile<COUNT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
 #ifdef RT_SEG_PROFILE
     if (!COUNT) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -260,11 +268,11 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
         }
     }
 #endif
-    if (F.tile_cost && lane == 0 && quarter <= 0) {
+    if (F.tile_cost && lane == 0 && part <= 0) {
         // log-scale cost key (4 mantissa bits, < 512): one cheap sort pass
-        // set; a split tile is charged four times its first quarter
+        // set; a split tile is charged its first part times the parts
         unsigned long long c64 = __builtin_amdgcn_s_memtime() - t0;
-        if (quarter == 0) c64 *= 4;
+        if (part == 0) c64 <<= 8 - pshift;
         const unsigned c = (unsigned)min(c64, 0xffffffffull);
         const unsigned e = c ? 31u - __clz(c) : 0u;
         F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
@@ -424,10 +432,10 @@ namespace rtk {
 
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
-    const int blocks = (F.num_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
+    const int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
     if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    else if (F.split_tiles > 0)
+    else if (F.split_tiles > 0 || F.split16_tiles > 0)
         hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (RT_MK_LEVELS && S.bvh4 && F.spp >= RT_MK_LEVELS_MIN_SPP)
         return launch_render_levels(S, F, stream);
