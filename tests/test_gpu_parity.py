@@ -305,3 +305,18 @@ def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
             assert np.array_equal(img.view(np.uint32), row.view(np.uint32)), kw
             assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == (sr.primary_rays, sr.shadow_rays,
                                                                              sr.reflection_rays), kw
+
+
+def test_split_sixteenths_of_large_shards_is_invisible(gpu_ctx, rt):
+    """Shards of 24,000-70,000 tiles (a 1/2 and a 1/4 shard of 1080p C3) run
+    only their slowest 1/4096 of tiles as sixteen one-pixel waves: same bits
+    and ray counts as row-major frames; the whole frame does not split."""
+    fr = rt.make("C3")
+    gpu_ctx.set_scene(fr.scene)
+    for kw in (dict(band_index=0, band_count=2, band_rows=8), dict(band_index=3, band_count=4, band_rows=8)):
+        row, sr = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
+        for _ in range(3):
+            img, st = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
+            assert np.array_equal(img.view(np.uint32), row.view(np.uint32)), kw
+            assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == (sr.primary_rays, sr.shadow_rays,
+                                                                             sr.reflection_rays), kw

@@ -1,5 +1,5 @@
 """Experiment check: a library variant's split frames equal row-major
-whole-tile frames bit for bit (C3 at 640x360 and 1/8 shards of 1080p).
+whole-tile frames bit for bit (C3 at 640x360, 1/8 and 1/4 shards of 1080p, the whole 1080p frame).
 
     python tools/split_check.py --lib s16_1024"""
 import argparse
@@ -22,7 +22,9 @@ def main():
     ctx = rt.Context(lib_path=lib)
     ok = True
     for fr, kw in ((rt.make("C3").with_resolution(640, 360), {}),
-                   (rt.make("C3"), dict(band_index=3, band_count=8, band_rows=8))):
+                   (rt.make("C3"), dict(band_index=3, band_count=8, band_rows=8)),
+                   (rt.make("C3"), dict(band_index=1, band_count=4, band_rows=8)),
+                   (rt.make("C3"), {})):
         ctx.set_scene(fr.scene)
         row, sr = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
         for _ in range(3):
