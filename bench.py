@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams consecutive frames alternate on: frames in flight, so one frame's slowest "
                          "tiles overlap the next frame's bulk (1 = one frame at a time)")
+    ap.add_argument("--gather-frames", type=int, default=0,
+                    help="N > 1: frames per RCCL gather (one collective per group of frames; 0 = --streams)")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--sim-bands", type=int, default=0,
                     help="experiment (one GPU, no gather): render only row band 0 of N, i.e. one rank's share "
@@ -143,26 +145,37 @@ def main():
     fr = rt.make(args.config)
     ctx = rt.Context(lib_path=os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", args.lib, "librt_mi355.so")
                      if args.lib else None)
-    stream = torch.cuda.current_stream()
+    # a created stream, current for the whole run: the null stream's handle is 0,
+    # which rt_set_stream reads as "the context's own stream" (non-blocking,
+    # unordered with torch's null stream and with RCCL's waits)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_scene(fr.scene)
     rx, ry = fr.plane.ResolutionX, fr.plane.ResolutionY
     R = 8
     band_count = world if not args.sim_bands else args.sim_bands
     local_rows = ctx.lib.rt_band_rows_local(ry, rank, band_count, R) if (dist_on or args.sim_bands) else ry
-    # Frames rotate over nbuf output buffers and `--streams` HIP streams (more
-    # than one stream = frames in flight, off by default).  N > 1: each
-    # buffer's shard is gathered to rank 0 over RCCL asynchronously (the NCCL
-    # stream waits for the buffer's render stream) while the next frame
-    # renders; rank 0 reassembles a frame when its buffer comes round again
-    # (or at the end).
+    # Frames rotate over `--streams` HIP streams (more than one = frames in
+    # flight).  N > 1: frames are gathered to rank 0 in groups of G
+    # (`--gather-frames`, default = streams): each rank's shards of a group
+    # sit back to back in one buffer, one RCCL gather per group (the NCCL
+    # stream waits for the group's render streams) moves them over xGMI while
+    # the other group renders, and rank 0 reassembles the whole group with one
+    # HIP launch (bands.assemble_frames: the stack is the shard of one tall
+    # image) before the group's buffers are reused.  One collective per G
+    # frames keeps rank 0's host cost per frame (a gather call is ~35 us of
+    # host time) below a 1/8 shard's frame time.
     nstreams = max(1, args.streams)
-    nbuf = max(nstreams, 2 if dist_on else 1)
     streams = [stream] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     # sharded frames travel as float RGB (RT_FLAG_OUT_RGB32F: the Color values
     # bit for bit without the constant alpha, 12 B/px): a quarter less to gather
     ch = 3 if dist_on else 4
-    outs = [torch.empty((local_rows, rx, ch), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    G = (args.gather_frames or nstreams) if dist_on else 1
+    ngroups = 2 if dist_on else max(1, -(-nstreams // G))
+    groups = [torch.empty((G, local_rows, rx, ch), dtype=torch.float32, device="cuda") for _ in range(ngroups)]
+    nbuf = G * ngroups
+    outs = [groups[b // G][b % G] for b in range(nbuf)]
     out = outs[0]
     nbytes = out.numel() * 4
     mode_flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET}.get(args.mode, 0)
@@ -170,65 +183,93 @@ def main():
         mode_flags |= rt.abi.RT_FLAG_OUT_RGB32F
     params = rt.frame_params(fr, band_index=rank if dist_on else 0, band_count=band_count, band_rows=R,
                              flags=mode_flags)
+    span = local_rows * world  # rows of one frame in the tall group image (>= ry)
     if dist_on:
-        gath = [torch.empty((world, local_rows, rx, ch), dtype=torch.float32, device="cuda") for _ in range(nbuf)] \
-            if rank == 0 else [None] * nbuf
-        images = [torch.empty((ry, rx, ch), dtype=torch.float32, device="cuda") for _ in range(nbuf)] \
-            if rank == 0 else [None] * nbuf
+        gath = [torch.empty((world, G * local_rows, rx, ch), dtype=torch.float32, device="cuda")
+                for _ in range(ngroups)] if rank == 0 else [None] * ngroups
+        gath_lists = [list(g.unbind(0)) for g in gath] if rank == 0 else [None] * ngroups
+        images = [torch.empty((G, span, rx, ch), dtype=torch.float32, device="cuda") for _ in range(ngroups)] \
+            if rank == 0 else [None] * ngroups
         if gloo:  # host staging buffers for the rehearsal backend
-            outs_h = [torch.empty((local_rows, rx, ch), dtype=torch.float32) for _ in range(nbuf)]
-            gath_h = [torch.empty((world, local_rows, rx, ch), dtype=torch.float32) for _ in range(nbuf)] \
-                if rank == 0 else [None] * nbuf
-    pending = [None] * nbuf
+            groups_h = [torch.empty((G * local_rows, rx, ch), dtype=torch.float32) for _ in range(ngroups)]
+            gath_h = [torch.empty((world, G * local_rows, rx, ch), dtype=torch.float32) for _ in range(ngroups)] \
+                if rank == 0 else [None] * ngroups
+            gath_h_lists = [list(g.unbind(0)) for g in gath_h] if rank == 0 else [None] * ngroups
+    pending = [None] * ngroups
+    freed = [torch.cuda.Event() for _ in range(ngroups)]
 
-    def begin_gather(b):
-        """Shard b -> rank 0 (RCCL gather over xGMI, async on the NCCL stream)."""
+    def begin_gather(g):
+        """Group g's shards -> rank 0 (RCCL gather over xGMI, async on the
+        NCCL stream, which waits for the current stream); the caller made the
+        current stream wait for every stream that rendered into the group."""
+        src = groups[g].view(G * local_rows, rx, ch)
         if gloo:
-            outs_h[b].copy_(outs[b])
-            src, dst_list = outs_h[b], (list(gath_h[b].unbind(0)) if rank == 0 else None)
+            groups_h[g].copy_(src)
+            pending[g] = dist.gather(groups_h[g], gath_h_lists[g] if rank == 0 else None, dst=0, async_op=True)
         else:
-            src, dst_list = outs[b], (list(gath[b].unbind(0)) if rank == 0 else None)
-        pending[b] = dist.gather(src, dst_list, dst=0, async_op=True)
+            pending[g] = dist.gather(src, gath_lists[g] if rank == 0 else None, dst=0, async_op=True)
 
-    def finish_gather(b):
-        """Wait for buffer b's gather (stream-level wait for RCCL) and let
-        rank 0 put its rows back in order with the HIP reassembly kernel."""
-        w = pending[b]
+    def finish_gather(g):
+        """Wait for group g's gather (stream-level wait for RCCL) and let rank
+        0 put the group's rows back in order with one HIP reassembly launch;
+        then the group's buffers are free (event `freed[g]`)."""
+        w = pending[g]
         if w is None:
             return
         w.wait()
-        pending[b] = None
+        pending[g] = None
         if rank == 0:
             if gloo:
-                gath[b].copy_(gath_h[b])
-            ctx.assemble_bands(gath[b].data_ptr(), rx, ry, world, R, images[b].data_ptr(), pixel_bytes=4 * ch,
-                               sync=False)
+                gath[g].copy_(gath_h[g])
+            ctx.assemble_bands(gath[g].data_ptr(), rx, G * span, world, R, images[g].data_ptr(),
+                               pixel_bytes=4 * ch, sync=False)
 
     # Frames are enqueued asynchronously (RT_FLAG_ASYNC): the host keeps the
     # stream fed and rt_finish returns the summed counters of the timed frames.
     aparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
                               flags=mode_flags | rt.abi.RT_FLAG_ASYNC)
     frame_no = [0]
+    last_frame = [0]
     cam_s, plane_s = rt.raytracing.camera_struct(fr.camera), rt.raytracing.plane_struct(fr.plane)
 
-    def step():
-        b = frame_no[0] % nbuf
-        sb = streams[b % nstreams]
+    def close_group(g, used):
+        """Gather group g once its `used` frames are enqueued."""
+        sb = streams[(used - 1) % nstreams]
         with torch.cuda.stream(sb):
-            ctx.set_stream(sb.cuda_stream)
-            finish_gather(b)  # buffer b's previous frame: gathered and reassembled; the buffer is free
-            ctx.render_device(cam_s, plane_s, aparams, outs[b].data_ptr(), nbytes)
-            if dist_on:
-                begin_gather(b)
+            for k in range(min(used, nstreams) - 1):
+                sb.wait_stream(streams[(used - 2 - k) % nstreams])
+            begin_gather(g)
+
+    def step():
+        f = frame_no[0]
+        b = f % nbuf
+        g, j = b // G, b % G
+        sb = streams[(j if dist_on else b) % nstreams]
+        last_frame[0] = f
+        ctx.set_stream(sb.cuda_stream)
+        if dist_on:
+            if j == 0:  # the group's previous gather: done and reassembled, buffers free
+                with torch.cuda.stream(sb):  # RCCL's wait targets the current stream
+                    finish_gather(g)
+                freed[g].record(sb)
+            else:
+                sb.wait_event(freed[g])
+        ctx.render_device(cam_s, plane_s, aparams, outs[b].data_ptr(), nbytes)
+        if dist_on and j == G - 1:
+            close_group(g, G)
         frame_no[0] += 1
 
     def drain():
-        for k in range(nbuf):
-            b = (frame_no[0] + k) % nbuf
-            sb = streams[b % nstreams]
-            with torch.cuda.stream(sb):
-                ctx.set_stream(sb.cuda_stream)
-                finish_gather(b)
+        if dist_on:
+            j = frame_no[0] % G
+            if j:  # a partial group: gather it as is and start the next frame on a fresh group
+                close_group((frame_no[0] % nbuf) // G, j)
+                frame_no[0] += G - j
+            for k in range(ngroups):
+                g = ((frame_no[0] % nbuf) // G + k) % ngroups
+                with torch.cuda.stream(stream):
+                    ctx.set_stream(stream.cuda_stream)
+                    finish_gather(g)
         ctx.set_stream(stream.cuda_stream)
 
     # counting launch (untimed): algorithmic work of this rank's frame
@@ -247,6 +288,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    host_s = time.perf_counter() - t0  # host time to enqueue the K frames
     drain()
     st = ctx.finish()
     ctx.set_stream(stream.cuda_stream)
@@ -281,10 +323,21 @@ def main():
             ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=mode_flags & ~rt.abi.RT_FLAG_OUT_RGB32F),
                               full.data_ptr(),
                               full.numel() * 4)
-            last = images[(frame_no[0] - 1) % nbuf]
+            lb = last_frame[0] % nbuf
+            last = images[lb // G][lb % G, :ry]
             same = bool(torch.equal(full[..., :ch].contiguous().view(torch.int32), last.view(torch.int32)))
             print(json.dumps({"verify_sharded_equals_single": same}), file=sys.stderr, flush=True)
             if not same:
+                ref = full[..., :ch].contiguous().view(torch.int32)
+                diag = {"last_frame": last_frame[0], "group": lb // G, "slot": lb % G,
+                        "images_equal": [[bool(torch.equal(images[g][k, :ry].view(torch.int32), ref))
+                                          for k in range(G)] for g in range(ngroups)]}
+                if world == 1:
+                    diag["shards_equal"] = [[bool(torch.equal(groups[g][k, :ry].view(torch.int32), ref))
+                                             for k in range(G)] for g in range(ngroups)]
+                    diag["gathered_equal"] = [[bool(torch.equal(gath[g][0, k * ry:(k + 1) * ry].view(torch.int32),
+                                                                ref)) for k in range(G)] for g in range(ngroups)]
+                print(json.dumps(diag), file=sys.stderr, flush=True)
                 raise SystemExit("sharded frame differs from the single-rank frame")
     if dist_on:
         t = torch.tensor([elapsed, float(rays), kernel_ms], dtype=torch.float64,
@@ -326,10 +379,13 @@ def main():
                                                         if dist_on else ""),
                 "rays_per_frame": rays // args.steps,
                 "frames_in_flight": nstreams,
+                "frames_per_gather": G if dist_on else None,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
                 # primary samples (W*H*spp of the frame, or of this band) per second
                 "msamples_per_s": rx * (local_rows if args.sim_bands else ry) * fr.spp * args.steps / elapsed / 1e6,
                 "end_to_end_ms_per_frame": e2e_ms,
+                # rank 0's host time per enqueued frame: near ms_per_step means host-bound
+                "host_enqueue_ms_per_frame": host_s / args.steps * 1e3,
             },
             "roofline": {
                 "bound": "hbm",

@@ -90,3 +90,20 @@ def test_band_partition_covers_rows_once(rt):
                                    bands.band_global_rows(H, r, n, 8), -1) for r in range(n)])
             img = bands.assemble(g[..., None, None], H, 8)
             assert np.array_equal(img[:, 0, 0], np.arange(H))
+
+
+def test_frame_group_reassembly_is_per_frame_reassembly(rt):
+    """bench.py gathers a group of frames per collective (each rank's shards
+    stacked frame after frame) and reassembles the group as one tall image;
+    every frame must come out as its own per-frame reassembly would."""
+    from unity_raytracer_amd import bands
+    rng = np.random.default_rng(7)
+    for H in (37, 1080):
+        for n in (1, 2, 3, 8):
+            for G in (1, 2, 4):
+                loc = bands.band_local_rows(H, n, 8)
+                shards = rng.integers(0, 1 << 30, size=(G, n, loc, 3, 2), dtype=np.int64)
+                group = np.concatenate([shards[j] for j in range(G)], axis=1)  # (n, G*loc, W, C)
+                got = bands.assemble_frames(group, H, G, 8)
+                for j in range(G):
+                    assert np.array_equal(got[j], bands.assemble(shards[j], H, 8)), (H, n, G, j)

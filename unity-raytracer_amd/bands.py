@@ -47,3 +47,19 @@ def assemble(gathered: np.ndarray, res_y: int, band_rows: int = 8) -> np.ndarray
     slot = blk // band_count
     ly = slot * band_rows + (gy - blk * band_rows)
     return gathered[band, ly]
+
+
+def assemble_frames(gathered: np.ndarray, res_y: int, frames: int, band_rows: int = 8) -> np.ndarray:
+    """(band_count, frames * local_rows, W, C): the shards of `frames` frames,
+    each rank's stacked frame after frame (one gather per frame group) ->
+    (frames, res_y, W, C).  local_rows is a multiple of band_rows, so the
+    stack is the block-cyclic shard of one tall image of frames * local_rows *
+    band_count rows in which frame j starts at row j * local_rows * band_count:
+    one reassembly (bench.py: rt_assemble_bands over the tall image) serves
+    the whole group."""
+    band_count, tall_local = gathered.shape[:2]
+    local_rows = tall_local // frames
+    assert local_rows * frames == tall_local and (band_count == 1 or local_rows % band_rows == 0)
+    span = local_rows * band_count
+    tall = assemble(gathered, frames * span, band_rows)
+    return tall.reshape(frames, span, *tall.shape[1:])[:, :res_y]
