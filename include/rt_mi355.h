@@ -212,7 +212,10 @@ void rt_destroy(rt_ctx *ctx);
 const char *rt_last_error(const rt_ctx *ctx);
 
 /* Use this HIP stream (hipStream_t passed as void*) for all device work;
- * null selects the context's own stream. */
+ * null selects the context's own stream (created non-blocking, so NOT the
+ * legacy null stream: a caller working on the null stream — e.g. torch's
+ * default stream, whose handle is 0 — must pass a created stream to order
+ * its own work with the library's). */
 int rt_set_stream(rt_ctx *ctx, void *hip_stream);
 
 /* Upload a scene: copies every array to HBM, computes Scene.AABB exactly as
