@@ -415,7 +415,10 @@ constexpr int kSplitDiv = RT_SPLIT_DIV;  // 1/kSplitDiv of the tiles (the slowes
 constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this many tiles
 constexpr int kSplit16MaxTiles = RT_SPLIT16_MAX_TILES;
 constexpr int kSplit16DivLarge = RT_SPLIT16_DIV_LARGE;
-constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
+#ifndef RT_LPT_PERIOD
+#define RT_LPT_PERIOD 16
+#endif
+constexpr int kLptPeriod = RT_LPT_PERIOD;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 
 // Sums the sharded ray/test counters on the host (the stream must be idle).
 int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
