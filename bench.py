@@ -278,6 +278,17 @@ def main():
     cst = ctx.render_device(fr.camera, fr.plane, cparams, out.data_ptr(), nbytes)
     bytes_per_launch = algorithmic_bytes(cst, rx, local_rows)
 
+    # setup, untimed: one frame on each stream before the W warmup steps.  A
+    # stream's first frame allocates its longest-first state in the library
+    # (device buffers, the sort's scratch), which blocks the host for
+    # milliseconds; with W < --streams that setup would otherwise land in
+    # the timed region (measured: 0.29 ms of host stall per timed frame at
+    # K = 20, W = 3).
+    for sb in streams:
+        ctx.set_stream(sb.cuda_stream)
+        ctx.render_device(cam_s, plane_s, aparams, out.data_ptr(), nbytes)
+    ctx.finish()
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     drain()
