@@ -12,6 +12,7 @@ namespace rtk {
 // Megakernel: one lane per sample, whole Whitted chain in one launch (trace.hip).
 // Longest-first tile order for the next frame (trace.hip).
 size_t tile_sort_scratch_bytes(int n);
+hipError_t launch_iota(int *p, int n, hipStream_t stream);
 hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const int *iota, int *order, int n,
                               void *scratch, size_t scratch_bytes, hipStream_t stream);
 

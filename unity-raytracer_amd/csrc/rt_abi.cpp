@@ -517,9 +517,8 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             HIP_OR_FAIL(ctx, ensure(ctx, ls->cost_sorted, n * 4));
             HIP_OR_FAIL(ctx, ensure(ctx, ls->order, n * 4));
             HIP_OR_FAIL(ctx, ensure(ctx, ls->scratch, rtk::tile_sort_scratch_bytes(F.num_tiles)));
-            std::vector<int> iota(n);
-            for (size_t i = 0; i < n; ++i) iota[i] = (int)i;
-            HIP_OR_FAIL(ctx, put(ctx, ls->iota, iota.data(), n));
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->iota, n * 4));
+            HIP_OR_FAIL(ctx, rtk::launch_iota((int *)ls->iota.p, F.num_tiles, ctx->stream));
             ls->key = key;
             ls->valid = false;
         }

@@ -453,6 +453,19 @@ size_t tile_sort_scratch_bytes(int n) {
     return bytes;
 }
 
+__global__ void iota_kernel(int *p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = i;
+}
+
+// The sort's identity payload, written on the device (a pageable host copy
+// would block the host on the stream's first frame).
+hipError_t launch_iota(int *p, int n, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p, n);
+    return hipGetLastError();
+}
+
 hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const int *iota, int *order, int n,
                               void *scratch, size_t scratch_bytes, hipStream_t stream) {
     size_t bytes = scratch_bytes;
