@@ -2,6 +2,7 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+    python bench.py --gpus N --in-process        # one process drives N GPUs (rt_create(N))
 
 One step = one frame of the BASELINE.json metric config (C3: 69,132-tri BVH
 scene, 1920x1080, 4 spp, depth 8) rendered through the C-ABI with the scene
@@ -10,14 +11,21 @@ frame's rows are block-cyclic sharded (band_index = rank) and the shards are
 gathered to rank 0 over RCCL and reassembled by a HIP kernel — the fixed
 frame is split, so scaling is "strong".  value = rays traced by all ranks
 (primary + shadow + reflection, counted on device) / max-over-ranks time.
+`--gpus N` without a launcher (no WORLD_SIZE) starts the N ranks itself
+(torch.distributed.run, before anything touches a GPU); a world size that
+differs from --gpus is an error.
 
 Rank 0 prints ONE JSON line with a roofline object for the trace kernel and
 a cpu_baseline measured with the C oracle (single-thread brute force, the
 reference's algorithm) on a bounded pixel sample of the same frame.
 """
 import argparse
+import hashlib
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,16 +49,112 @@ METRIC = "Mrays/sec + ms/frame at 1920x1080, 4spp, depth 8; 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
 
 
-def algorithmic_bytes(st, res_x, local_rows):
-    """B = 32*N_box + 36*N_tri + 16*N_sph + 16*N_hit + 16*W*H."""
+# Issue peaks for the SQ-counter rooflines (MI355X_MICROARCH.md "Chip-level
+# parameters" / "Wave scheduling"): 256 CUs x 4 SIMDs, 2.4 GHz; a wave64 VALU
+# instruction occupies its SIMD-32 for 2 cycles; one scalar unit per CU
+# issues at most one SALU instruction per cycle.
+CLOCK_HZ = 2.4e9
+VALU_PEAK = 256 * 4 * CLOCK_HZ / 2 / 1e9  # G wave-instructions/s
+SALU_PEAK = 256 * CLOCK_HZ / 1e9          # G instructions/s
+
+
+def logical_bytes(st, res_x, local_rows):
+    """B = 32*N_box + 36*N_tri + 16*N_sph + 16*N_hit + 16*W*H
+    (every per-ray node/primitive test priced as if fetched from HBM)."""
     return (32 * st.box_tests + 36 * st.triangle_tests + 16 * st.sphere_tests
             + 16 * st.shading_fetches + 16 * res_x * local_rows)
 
 
+def lib_sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def load_pmc(config, lib_path):
+    """Per-launch PMC counters of the trace kernel (profiles/pmc_<config>.json,
+    written by tools/pmc_round.sh + tools/pmc_summary.py on the GPU box).  Used
+    only when it was measured with the library this run loads (sha256 of the
+    .so), so the counters describe the code that ran."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(p):
+        return None, "missing"
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None, "unreadable"
+    if d.get("lib_sha256") != lib_sha256(lib_path):
+        return None, "stale (measured with another build of the library)"
+    return d, "fresh"
+
+
+def roofline(pmc, pmc_state, kernel_name, avg_kernel_s, logical):
+    """Roofline object of the trace kernel.  HBM: counter-measured bytes per
+    launch (TCC_EA0 read/write requests) over the live kernel time; issue:
+    SQ_INSTS_VALU / SQ_INSTS_SALU per launch over the same time against the
+    chip's issue rates.  `bound` is the most utilised of the three; the
+    §8(d) per-ray byte model is reported as logical_bytes (it counts node and
+    triangle re-reads that L2 / Infinity Cache serve, so it exceeds HBM peak)."""
+    out = {"kernel": kernel_name, "avg_kernel_ms": avg_kernel_s * 1e3, "pmc": pmc_state,
+           "logical_bytes_per_launch": logical, "logical_gbs": logical / avg_kernel_s / 1e9}
+    legs = {}
+    if pmc:
+        hbm = pmc.get("hbm_bytes_per_launch")
+        c = pmc.get("counters", {})
+        if hbm:
+            a = hbm / avg_kernel_s / 1e9
+            legs["hbm"] = {"achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
+                           "read_bytes": pmc.get("read_bytes_per_launch"),
+                           "write_bytes": pmc.get("write_bytes_per_launch")}
+        if c.get("SQ_INSTS_VALU"):
+            a = c["SQ_INSTS_VALU"] / avg_kernel_s / 1e9
+            legs["valu_issue"] = {"achieved": a, "peak": VALU_PEAK, "unit": "Gwave-inst/s", "frac": a / VALU_PEAK}
+        if c.get("SQ_INSTS_SALU"):
+            a = c["SQ_INSTS_SALU"] / avg_kernel_s / 1e9
+            legs["salu_issue"] = {"achieved": a, "peak": SALU_PEAK, "unit": "Ginst/s", "frac": a / SALU_PEAK}
+        if c.get("SQ_WAVE_CYCLES"):
+            tot = c["SQ_WAVE_CYCLES"]
+            out["wave_time_split"] = {k: c.get(v, 0.0) / tot for k, v in
+                                      (("issuing", "SQ_ACTIVE_INST_ANY"), ("waiting_memory", "SQ_WAIT_ANY"),
+                                       ("waiting_issue", "SQ_WAIT_INST_ANY"))}
+        out["traffic"] = hbm
+    else:
+        out["traffic"] = None
+    if legs:
+        bound = max(legs, key=lambda k: legs[k]["frac"])
+        out.update({"bound": bound, **{k: legs[bound][k] for k in ("achieved", "peak", "unit", "frac")}})
+        out.update(legs)
+    else:  # no counters for this build: the HBM leg cannot be priced
+        out.update({"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None})
+    return out
+
+
+def host_facts():
+    """Host core count and CPU model (BASELINE.md CPU-baseline plan)."""
+    model = platform.processor() or ""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = os.cpu_count() or 1
+    return {"nproc": os.cpu_count() or 1, "affinity_cpus": affinity, "cpu_model": model}
+
+
 def cpu_baseline(rt, fr, budget_s):
-    """Single-thread brute-force oracle (the reference's algorithm, which is
-    single-threaded Mono C#) on seeded random pixels of the same frame,
-    until budget_s of CPU time: returns Mrays/s (same ray accounting)."""
+    """The C oracle (brute force, the reference's algorithm) on seeded random
+    pixels of the same frame: 1 thread (the reference is single-threaded
+    Mono) for budget_s, then OpenMP over every host core this job is given
+    (the affinity mask, capped by OMP_NUM_THREADS: the GPU box grants a
+    one-GPU job 16 cores of a larger machine) for budget_s / 3.  Mrays/s with
+    the same ray accounting as the GPU line."""
     orc = _rt_pkg.load_oracle()
     rng = np.random.default_rng(20250101)
     total = fr.plane.ResolutionX * fr.plane.ResolutionY
@@ -63,37 +167,66 @@ def cpu_baseline(rt, fr, budget_s):
         secs += time.perf_counter() - t0
         rays += c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
         pixels += batch
-    # the same code on the host cores the box gives this job (OpenMP over pixels)
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
-    mrays, msecs = 0, 0.0
+    facts = host_facts()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(facts["affinity_cpus"], omp) if omp else facts["affinity_cpus"])
+    mrays, msecs, mpix = 0, 0.0, 0
     while msecs < budget_s / 3:
         idx = rng.integers(0, total, 64 * threads).astype(np.int32)
         t0 = time.perf_counter()
         _, c = orc.render_pixels(fr, idx, threads=threads)
         msecs += time.perf_counter() - t0
         mrays += c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
+        mpix += len(idx)
     return {
         "value": rays / secs / 1e6,
         "unit": "Mrays/s",
         "cores": 1,
         "kind": "port",
         "sample": f"{pixels} seeded random pixels of {fr.name} ({fr.spp} spp, depth {fr.max_bounces}), "
-                  f"{rays} rays in {secs:.1f} s, brute-force C oracle (oracle/rt_oracle.c), 1 thread "
-                  f"(the reference is single-threaded)",
+                  f"{rays} rays in {secs:.1f} s, brute-force C oracle (oracle/rt_oracle.c, gcc -O3 "
+                  f"-march=x86-64-v2 -ffp-contract=off), 1 thread (the reference is single-threaded)",
         "all_cores_value": mrays / msecs / 1e6,
         "all_cores_threads": threads,
+        "all_cores_sample": f"{mpix} seeded random pixels, {mrays} rays in {msecs:.1f} s",
+        **facts,
     }
 
 
-def load_traffic(config):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
-    if os.path.exists(p):
-        try:
-            return json.load(open(p)).get("hbm_bytes_per_launch")
-        except Exception:
-            return None
-    return None
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """--gpus N without a launcher: run this script as N ranks under
+    torch.distributed.run (a child process: nothing here has touched a GPU)
+    and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def orbit_cameras(rt, cam0, n, yaw_deg=12.0):
+    """n cameras swinging +-yaw_deg about the y axis through the scene centre
+    (the origin), looking at it: RayTracingSetup.Update's basis (:175-181) for
+    a moving Transform.  Left-handed like Unity: right = up x forward."""
+    p0 = np.array(cam0.Position, np.float64)
+    r = float(np.linalg.norm(p0))
+    out = []
+    for k in range(n):
+        th = np.radians(yaw_deg) * np.sin(2 * np.pi * k / max(1, n))
+        pos = np.array([-r * np.sin(th), p0[1], -r * np.cos(th)])
+        fwd = -pos / np.linalg.norm(pos)
+        up_w = np.array([0.0, 1.0, 0.0])
+        right = np.cross(up_w, fwd)
+        right /= np.linalg.norm(right)
+        up = np.cross(fwd, right)
+        out.append(rt.raytracing.camera_struct(rt.CameraData(tuple(pos), tuple(fwd), tuple(right), tuple(up))))
+    return out
 
 
 def main():
@@ -120,15 +253,40 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: ranks may share a GPU, "
                          "gather through host memory)")
+    ap.add_argument("--in-process", action="store_true",
+                    help="one process drives --gpus GPUs through one multi-device context (rt_create(N): row "
+                         "bands per GPU, RCCL gather inside the library), as a Unity host would")
+    ap.add_argument("--devices", default="",
+                    help="--in-process: explicit device list, e.g. 0,0,0 (logical shards on one GPU, peer copies)")
+    ap.add_argument("--moving-frames", type=int, default=64,
+                    help="N = 1: also time this many frames of an orbiting camera (0 = skip)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="test hook: form the process group, report rank/world on stderr, exit (no GPU work)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.in_process:
+        raise SystemExit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
+    if args.in_process and world != 1:
+        raise SystemExit("--in-process runs in one process (no launcher)")
+    if not args.in_process and world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     gloo = args.dist_backend == "gloo"
     dist_on = world > 1 or args.force_dist
+    if args.launch_check:
+        if dist_on:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            print(json.dumps({"launch_check": True, "rank": dist.get_rank(), "world": dist.get_world_size()}),
+                  file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+        else:
+            print(json.dumps({"launch_check": True, "rank": 0, "world": 1}), file=sys.stderr, flush=True)
+        return
+    if args.in_process:
+        return main_in_process(args)
     ndev = torch.cuda.device_count()
     device = local_rank % ndev if gloo else local_rank
     torch.cuda.set_device(device)
@@ -140,11 +298,13 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", device))
+        world = dist.get_world_size()  # the ranks that actually joined
 
     rt = _rt_pkg.load()
     fr = rt.make(args.config)
-    ctx = rt.Context(lib_path=os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", args.lib, "librt_mi355.so")
-                     if args.lib else None)
+    lib_path = (os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", args.lib, "librt_mi355.so")
+                if args.lib else rt.abi.LIB_PATH)
+    ctx = rt.Context(lib_path=lib_path if args.lib else None)
     # a created stream, current for the whole run: the null stream's handle is 0,
     # which rt_set_stream reads as "the context's own stream" (non-blocking,
     # unordered with torch's null stream and with RCCL's waits)
@@ -240,7 +400,7 @@ def main():
                 sb.wait_stream(streams[(used - 2 - k) % nstreams])
             begin_gather(g)
 
-    def step():
+    def step(cam=None):
         f = frame_no[0]
         b = f % nbuf
         g, j = b // G, b % G
@@ -254,7 +414,7 @@ def main():
                 freed[g].record(sb)
             else:
                 sb.wait_event(freed[g])
-        ctx.render_device(cam_s, plane_s, aparams, outs[b].data_ptr(), nbytes)
+        ctx.render_device(cam or cam_s, plane_s, aparams, outs[b].data_ptr(), nbytes)
         if dist_on and j == G - 1:
             close_group(g, G)
         frame_no[0] += 1
@@ -272,11 +432,13 @@ def main():
                     finish_gather(g)
         ctx.set_stream(stream.cuda_stream)
 
-    # counting launch (untimed): algorithmic work of this rank's frame
+    # counting launch (untimed): algorithmic work of this rank's frame, and
+    # the camera samples the Scene.AABB gate rejects before any object test
     cparams = rt.frame_params(fr, band_index=params.band_index, band_count=band_count, band_rows=R,
                               flags=rt.abi.RT_FLAG_COUNT_TESTS | mode_flags)
     cst = ctx.render_device(fr.camera, fr.plane, cparams, out.data_ptr(), nbytes)
-    bytes_per_launch = algorithmic_bytes(cst, rx, local_rows)
+    logical = logical_bytes(cst, rx, local_rows)
+    scene_misses = int(cst.primary_scene_misses)
 
     # setup, untimed: one frame on each stream before the W warmup steps.  A
     # stream's first frame allocates its longest-first state in the library
@@ -314,9 +476,32 @@ def main():
         ctx.render_device(fr.camera, fr.plane, aparams, out.data_ptr(), nbytes)
     kernel_ms = ctx.finish().kernel_ms
 
+    # a moving camera (N = 1): every frame from another viewpoint, so the
+    # longest-first order always comes from earlier, different frames
+    moving = None
+    if not dist_on and not args.sim_bands and args.moving_frames > 0:
+        cams = orbit_cameras(rt, fr.camera, args.moving_frames)
+        for c in cams[:8]:  # warm the orbit's first views
+            step(c)
+        drain()
+        ctx.finish()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for c in cams:
+            step(c)
+        drain()
+        mst = ctx.finish()
+        torch.cuda.synchronize()
+        mel = time.perf_counter() - t1
+        mrays = mst.primary_rays + mst.shadow_rays + mst.reflection_rays
+        moving = {"frames": len(cams), "yaw_deg": 12.0, "mrays_per_s": mrays / mel / 1e6,
+                  "ms_per_frame": mel / len(cams) * 1e3, "rays_per_frame": mrays // len(cams)}
+
     # end-to-end rt_render (synchronous, host Color[] output: includes the D2H
-    # copy over PCIe), N = 1 only; reported beside `value`, never as it
+    # copy over PCIe, overlapped with the rendering by row slabs), N = 1 only;
+    # reported beside `value`, never as it
     e2e_ms = None
+    d2h_ms = None
     if not dist_on and not args.sim_bands and rank == 0:
         host = np.empty((ry, rx, 4), dtype=np.float32)
         ctx.set_stream(stream.cuda_stream)
@@ -326,6 +511,16 @@ def main():
             ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=mode_flags), out=host)
             ts.append(time.perf_counter() - t1)
         e2e_ms = float(np.median(ts[1:])) * 1e3
+        # the 33 MB device-to-host copy alone into the same pageable buffer
+        src = torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda")
+        hs = torch.from_numpy(host)
+        cs = []
+        for _ in range(6):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            hs.copy_(src)
+            cs.append(time.perf_counter() - t1)
+        d2h_ms = float(np.median(cs[1:])) * 1e3
 
     if dist_on and args.verify:
         # the assembled frame must be bit-identical to a single-rank frame
@@ -351,7 +546,7 @@ def main():
                 print(json.dumps(diag), file=sys.stderr, flush=True)
                 raise SystemExit("sharded frame differs from the single-rank frame")
     if dist_on:
-        t = torch.tensor([elapsed, float(rays), kernel_ms], dtype=torch.float64,
+        t = torch.tensor([elapsed, float(rays), kernel_ms, float(scene_misses)], dtype=torch.float64,
                          device="cpu" if gloo else "cuda")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -359,13 +554,16 @@ def main():
         elapsed = float(tmax[0])
         rays = int(t[1])
         kernel_ms_max = float(tmax[2])
+        scene_misses = int(t[3])
     else:
         kernel_ms_max = kernel_ms
 
     if rank == 0:
         avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's own trace kernel, HIP events
-        traffic = load_traffic(args.config)
-        achieved = bytes_per_launch / avg_kernel_s / 1e9
+        pmc, pmc_state = load_pmc(args.config, lib_path)
+        kname = {"megakernel": "render_kernel<false, false>", "packet": "render_packet_kernel<false, 1>"}.get(
+            args.mode, "wavefront passes (sum)")
+        rays_per_frame = rays // args.steps
         line = {
             "metric": METRIC,
             "value": rays / elapsed / 1e6,
@@ -388,32 +586,24 @@ def main():
                 "triangles": fr.scene.triangle_count,
                 "parallelism": f"row-bands x{world}" + ((" + gloo gather (rehearsal)" if gloo else " + RCCL gather")
                                                         if dist_on else ""),
-                "rays_per_frame": rays // args.steps,
+                "rays_per_frame": rays_per_frame,
+                # camera samples that end at the Scene.AABB gate (one slab test,
+                # Scene.cs:54) and the rays that enter the scene
+                "rays_trivial_miss": scene_misses,
+                "rays_in_scene": rays_per_frame - scene_misses,
+                "mrays_per_s_in_scene": (rays_per_frame - scene_misses) * args.steps / elapsed / 1e6,
                 "frames_in_flight": nstreams,
                 "frames_per_gather": G if dist_on else None,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
                 # primary samples (W*H*spp of the frame, or of this band) per second
                 "msamples_per_s": rx * (local_rows if args.sim_bands else ry) * fr.spp * args.steps / elapsed / 1e6,
                 "end_to_end_ms_per_frame": e2e_ms,
+                "d2h_copy_ms_per_frame": d2h_ms,
+                "moving_camera": moving,
                 # rank 0's host time per enqueued frame: near ms_per_step means host-bound
                 "host_enqueue_ms_per_frame": host_s / args.steps * 1e3,
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": {"megakernel": "render_kernel<false>", "packet": "render_packet_kernel<false,1>"}.get(
-                    args.mode, "wavefront passes (sum)"),
-                "bytes_per_launch": bytes_per_launch,
-                "avg_kernel_ms": avg_kernel_s * 1e3,
-                # rocprof-measured HBM bytes (PMC, profiles/pmc_<config>.json) per
-                # launch over the same launch time: the bandwidth actually drawn
-                "traffic_gbs": (traffic / avg_kernel_s / 1e9) if traffic else None,
-                "traffic_frac": (traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBS) if traffic else None,
-            },
+            "roofline": roofline(pmc, pmc_state, kname, avg_kernel_s, logical),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(rt, fr, args.cpu_seconds)
@@ -421,6 +611,96 @@ def main():
     ctx.close()
     if dist_on:
         dist.destroy_process_group()
+
+
+def main_in_process(args):
+    """One process, one multi-device context (rt_create(N) / rt_create_devices):
+    the library renders row bands on every GPU, gathers them to device 0
+    (RCCL send/recv) and reassembles — the path a Unity host takes.  Frames
+    rotate over --streams streams of device 0 with RT_FLAG_ASYNC."""
+    rt = _rt_pkg.load()
+    fr = rt.make(args.config)
+    devices = [int(d) for d in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    torch.cuda.set_device(devices[0])
+    ctx = rt.Context(devices=devices)
+    info = ctx.device_info()
+    streams = [torch.cuda.Stream() for _ in range(max(1, args.streams))]
+    torch.cuda.set_stream(streams[0])
+    ctx.set_stream(streams[0].cuda_stream)
+    t_scene = time.perf_counter()
+    ctx.set_scene(fr.scene)
+    scene_s = time.perf_counter() - t_scene
+    rx, ry = fr.plane.ResolutionX, fr.plane.ResolutionY
+    outs = [torch.empty((ry, rx, 4), dtype=torch.float32, device="cuda") for _ in streams]
+    nbytes = outs[0].numel() * 4
+    cam_s, plane_s = rt.raytracing.camera_struct(fr.camera), rt.raytracing.plane_struct(fr.plane)
+    aparams = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC)
+    cparams = rt.frame_params(fr, flags=rt.abi.RT_FLAG_COUNT_TESTS)
+    cst = ctx.render_device(cam_s, plane_s, cparams, outs[0].data_ptr(), nbytes)
+    frame = [0]
+
+    def step():
+        k = frame[0] % len(streams)
+        ctx.set_stream(streams[k].cuda_stream)
+        ctx.render_device(cam_s, plane_s, aparams, outs[k].data_ptr(), nbytes)
+        frame[0] += 1
+
+    for _ in range(len(streams) + args.warmup):
+        step()
+    ctx.finish()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    host_s = time.perf_counter() - t0
+    st = ctx.finish()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    rays = st.primary_rays + st.shadow_rays + st.reflection_rays
+    verified = None
+    if args.verify:
+        single = rt.Context()
+        single.set_scene(fr.scene)
+        ref = torch.empty_like(outs[0])
+        single.render_device(cam_s, plane_s, rt.frame_params(fr), ref.data_ptr(), nbytes)
+        ctx.set_stream(streams[0].cuda_stream)
+        ctx.render_device(cam_s, plane_s, rt.frame_params(fr), outs[0].data_ptr(), nbytes)
+        verified = bool(torch.equal(outs[0].view(torch.int32), ref.view(torch.int32)))
+        print(json.dumps({"verify_sharded_equals_single": verified}), file=sys.stderr, flush=True)
+        single.close()
+        if not verified:
+            raise SystemExit("multi-device frame differs from the single-device frame")
+    n_gpus = len(set(devices))
+    line = {
+        "metric": METRIC,
+        "value": rays / elapsed / 1e6,
+        "unit": "Mrays/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{fr.name}: {fr.scene.triangle_count}-triangle BVH scene, {rx}x{ry}, {fr.spp} spp, "
+                        f"depth {fr.max_bounces}",
+            "resolution": f"{rx}x{ry}", "spp": fr.spp, "depth": fr.max_bounces,
+            "parallelism": f"in-process row-bands x{info['num_devices']} on devices {info['devices']} + "
+                           + {0: "no gather", 1: "peer-copy gather", 2: "RCCL gather"}[info["gather"]],
+            "rays_per_frame": rays // args.steps,
+            "rays_trivial_miss": int(cst.primary_scene_misses),
+            "frames_in_flight": len(streams),
+            "kernel_ms_per_frame": st.kernel_ms / args.steps,
+            "host_enqueue_ms_per_frame": host_s / args.steps * 1e3,
+            "set_scene_ms": scene_s * 1e3,
+            "verified": verified,
+        },
+    }
+    print(json.dumps(line), flush=True)
+    ctx.close()
 
 
 if __name__ == "__main__":

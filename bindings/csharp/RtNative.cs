@@ -101,6 +101,15 @@ namespace RayTracer.Native
     {
         public ulong PrimaryRays, ShadowRays, ReflectionRays, BoxTests, TriangleTests, SphereTests, ShadingFetches;
         public double KernelMs, TotalMs;
+        public ulong PrimarySceneMisses;
+    }
+
+    // rt_device_info: the GPUs one context drives (rt_create(N > 1)).
+    [StructLayout(LayoutKind.Sequential)]
+    public struct RtDeviceInfo
+    {
+        public int NumDevices, Gather;
+        [MarshalAs(UnmanagedType.ByValArray, SizeConst = 16)] public int[] Devices;
     }
 
     [StructLayout(LayoutKind.Sequential)]
@@ -126,7 +135,14 @@ namespace RayTracer.Native
                          FlagAsync = 32, FlagRowOrder = 64;
 
         [DllImport(Lib)] public static extern int rt_abi_version();
+        public const int GatherNone = 0, GatherPeerCopy = 1, GatherRccl = 2;
+
+        // numGpus > 1: one context renders every frame on GPUs 0..numGpus-1
+        // (row bands, RCCL gather to GPU 0) — the same Color[] as one GPU.
         [DllImport(Lib)] public static extern int rt_create(out IntPtr ctx, int numGpus);
+        [DllImport(Lib)] public static extern int rt_create_devices(out IntPtr ctx, [In] int[] devices, int numDevices,
+                                                                   int gather);
+        [DllImport(Lib)] public static extern int rt_get_device_info(IntPtr ctx, out RtDeviceInfo info);
         [DllImport(Lib)] public static extern void rt_destroy(IntPtr ctx);
         [DllImport(Lib)] public static extern IntPtr rt_last_error(IntPtr ctx);
         [DllImport(Lib)] public static extern int rt_set_stream(IntPtr ctx, IntPtr hipStream);

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum rt_status {
@@ -175,8 +175,12 @@ typedef struct rt_stats {
     uint64_t triangle_tests;   /* Möller–Trumbore tests      (RT_FLAG_COUNT_TESTS) */
     uint64_t sphere_tests;     /* ray/sphere tests           (RT_FLAG_COUNT_TESTS) */
     uint64_t shading_fetches;  /* closest hits shaded (normal + material fetch)    */
-    double kernel_ms;          /* device time of the trace kernel(s)              */
+    double kernel_ms;          /* device time of the trace kernel(s); a multi-GPU
+                                  frame: the slowest device's                      */
     double total_ms;           /* wall time of the whole call                     */
+    uint64_t primary_scene_misses; /* camera samples rejected by the Scene.AABB gate
+                                      (Scene.cs:54) before any object test
+                                      (RT_FLAG_COUNT_TESTS)                         */
 } rt_stats;
 
 /* Closest-hit record, IntersectionResult (Data/Collision/IntersectionResult.cs:3-7)
@@ -199,10 +203,41 @@ typedef struct rt_ctx rt_ctx;
 /* ABI version of the loaded library (== RT_ABI_VERSION it was built with). */
 int32_t rt_abi_version(void);
 
-/* Create a context on the calling thread's current HIP device.  num_gpus
- * must be 1 (one context per GPU; multi-GPU frames shard rows with
- * rt_render_params.band_index/band_count across one process per GPU). */
+/* Create a context.  num_gpus == 1: on the calling thread's current HIP
+ * device.  num_gpus == N > 1: one context driving devices 0..N-1 of this
+ * process from the calling thread (a Unity-loaded .so cannot launch one
+ * process per GPU): the scene is replicated on every device
+ * and each rt_render / rt_render_device frame is split into block-cyclic
+ * row bands (8-row blocks, block b -> device b mod N, the pixels are
+ * independent: RayTracingSetup.cs:288-301), rendered concurrently, gathered
+ * to device 0 over xGMI by RCCL (ncclSend/ncclRecv in one group; peer copies
+ * when RCCL is unavailable), put back in row order on device 0 and, for
+ * rt_render, copied to the caller's Color[].  Frames are bit-identical to a
+ * one-device frame. */
 int rt_create(rt_ctx **out_ctx, int32_t num_gpus);
+
+/* Transport of a multi-device context's band gather. */
+#define RT_GATHER_NONE 0       /* one device                                            */
+#define RT_GATHER_PEER_COPY 1  /* hipMemcpyPeerAsync from every device into device 0   */
+#define RT_GATHER_RCCL 2       /* ncclSend/ncclRecv (one ncclGroupStart/End per frame)   */
+
+/* rt_create with an explicit device list (devices[0] is the root that
+ * receives the frame).  A device may appear more than once: its entries are
+ * separate logical shards on that GPU (testing the multi-device path on one
+ * GPU; the gather then uses peer copies).  gather: RT_GATHER_RCCL (default
+ * for distinct devices when 0 is passed) or RT_GATHER_PEER_COPY.  With
+ * RT_GATHER_RCCL even a one-device context routes its band through an RCCL
+ * self send/receive. */
+int rt_create_devices(rt_ctx **out_ctx, const int32_t *devices, int32_t num_devices, int32_t gather);
+
+/* What a context drives. */
+typedef struct rt_device_info {
+    int32_t num_devices;      /* members (shards per frame)                    */
+    int32_t gather;           /* RT_GATHER_*                                   */
+    int32_t devices[16];      /* HIP device ids of the first 16 members         */
+} rt_device_info;
+
+int rt_get_device_info(const rt_ctx *ctx, rt_device_info *info);
 
 /* Destroy a context (null is a no-op). */
 void rt_destroy(rt_ctx *ctx);
@@ -211,7 +246,10 @@ void rt_destroy(rt_ctx *ctx);
  * when ctx is null).  Never null; valid until the next call on ctx. */
 const char *rt_last_error(const rt_ctx *ctx);
 
-/* Use this HIP stream (hipStream_t passed as void*) for all device work;
+/* Use this HIP stream (hipStream_t passed as void*) for all device work
+ * (a multi-device context: device 0's work; the other devices use streams of
+ * their own, one per stream device 0 is given, so frames in flight stay
+ * independent);
  * null selects the context's own stream (created non-blocking, so NOT the
  * legacy null stream: a caller working on the null stream — e.g. torch's
  * default stream, whose handle is 0 — must pass a created stream to order
@@ -279,7 +317,10 @@ int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t 
  * of rt_pixel_bytes(flags) bytes — by default 4 floats (row-major, y = 0 is
  * the top row, alpha = 1), i.e. PixelColors.  When band_count > 1, only this
  * shard's rows are rendered and out_rgba receives the shard's compact
- * buffer (rt_band_rows_local rows). */
+ * buffer (rt_band_rows_local rows); on a multi-device context such a frame
+ * runs on device 0 only.  The device-to-host copy is overlapped with the
+ * rendering: the frame is rendered in row slabs and each finished slab is
+ * copied (through pinned staging) while the next ones render. */
 int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
               const rt_render_params *params, void *out_rgba, rt_stats *stats);
 

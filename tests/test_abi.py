@@ -23,7 +23,8 @@ def test_header_declares_expected_entry_points():
     names = _declared_functions()
     for n in ("rt_create", "rt_destroy", "rt_set_scene", "rt_render", "rt_render_device",
               "rt_last_error", "rt_intersect_rays", "rt_assemble_bands", "rt_abi_version",
-              "rt_set_scene_ex", "rt_get_scene_info", "rt_set_scene_source", "rt_update_mesh_transforms"):
+              "rt_set_scene_ex", "rt_get_scene_info", "rt_set_scene_source", "rt_update_mesh_transforms",
+              "rt_create_devices", "rt_get_device_info"):
         assert n in names
 
 
@@ -45,7 +46,7 @@ def test_ctypes_layouts(rt):
     sizes = {
         a.rt_float3: 12, a.rt_triangle: 36, a.rt_sphere: 16, a.rt_aabb: 24, a.rt_material: 56,
         a.rt_point_light: 24, a.rt_camera: 48, a.rt_scene_info: 32, a.rt_mesh_source: 152, a.rt_image_plane: 20, a.rt_mesh: 88, a.rt_hit: 16,
-        a.rt_ray: 24, a.rt_render_params: 40, a.rt_stats: 72,
+        a.rt_ray: 24, a.rt_render_params: 40, a.rt_stats: 80, a.rt_device_info: 72,
     }
     for t, s in sizes.items():
         assert C.sizeof(t) == s, t.__name__
@@ -59,10 +60,11 @@ def test_c_layouts_match(tmp_path):
 #include <stddef.h>
 #include "rt_mi355.h"
 int main(void){
- printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_mesh),
+ printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_mesh),
    sizeof(rt_scene_desc), sizeof(rt_render_params), sizeof(rt_stats), offsetof(rt_scene_desc, ambient_radiance),
    offsetof(rt_mesh, aabb), offsetof(rt_stats, kernel_ms), sizeof(rt_mesh_source),
-   offsetof(rt_mesh_source, local_to_world), offsetof(rt_mesh_source, material), sizeof(rt_scene_info));
+   offsetof(rt_mesh_source, local_to_world), offsetof(rt_mesh_source, material), sizeof(rt_scene_info),
+   offsetof(rt_stats, primary_scene_misses), sizeof(rt_device_info));
  return 0; }''')
     exe = tmp_path / "l"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(prog)], check=True)
@@ -72,7 +74,8 @@ int main(void){
     want = [C.sizeof(a.rt_material), C.sizeof(a.rt_mesh), C.sizeof(a.rt_scene_desc), C.sizeof(a.rt_render_params),
             C.sizeof(a.rt_stats), a.rt_scene_desc.ambient_radiance.offset, a.rt_mesh.aabb.offset,
             a.rt_stats.kernel_ms.offset, C.sizeof(a.rt_mesh_source), a.rt_mesh_source.local_to_world.offset,
-            a.rt_mesh_source.material.offset, C.sizeof(a.rt_scene_info)]
+            a.rt_mesh_source.material.offset, C.sizeof(a.rt_scene_info), a.rt_stats.primary_scene_misses.offset,
+            C.sizeof(a.rt_device_info)]
     assert vals == want
 
 
@@ -96,5 +99,5 @@ def test_pixel_bytes_per_format(rt):
         [16, 12, 8, 4]
     import re
     hdr = open(os.path.join(ROOT, "include", "rt_mi355.h")).read()
-    for name, val in re.findall(r"#define (RT_FLAG_\w+)\s+(\d+)", hdr):
+    for name, val in re.findall(r"#define (RT_(?:FLAG|GATHER|BUILD)_\w+)\s+(\d+)", hdr):
         assert getattr(a, name) == int(val), name

@@ -73,3 +73,24 @@ def test_bench_gloo_two_ranks_one_gpu():
     assert _verified(p.stderr), p.stderr[-3000:]
     d = _metric_line(p.stdout)
     assert d["n_gpus"] == 2 and d["config"]["frames_per_gather"] == 2
+
+
+def test_bench_spawns_gloo_ranks_without_launcher():
+    """`bench.py --gpus 2` with no launcher starts its own two ranks."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "4", "--warmup", "1",
+                        "--dist-backend", "gloo", "--verify", "--no-cpu-baseline", "--gather-frames", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    assert _verified(p.stderr), p.stderr[-3000:]
+    assert _metric_line(p.stdout)["n_gpus"] == 2
+
+
+def test_bench_in_process_multi_device():
+    """One process, one multi-device context (logical shards on GPU 0): the
+    library's own band gather, verified against a one-device frame."""
+    p = _run([sys.executable, "bench.py", "--in-process", "--devices", "0,0,0", "--steps", "4", "--warmup", "1",
+              "--verify"], timeout=240)
+    assert _verified(p.stderr), p.stderr[-3000:]
+    d = _metric_line(p.stdout)
+    assert "peer-copy" in d["config"]["parallelism"] and d["value"] > 0

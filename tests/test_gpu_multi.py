@@ -1,0 +1,145 @@
+"""Multi-GPU inside the drop-in library: one context drives
+several devices (rt_create(N) / rt_create_devices), renders block-cyclic row
+bands on each, gathers them to device 0 (RCCL send/recv or peer copies) and
+reassembles.  On a one-GPU box the same path runs as N logical shards on
+device 0 (peer copies), and the RCCL transport as a one-device group whose
+band travels through an RCCL self send/receive; with >= N GPUs visible, the
+real N-device RCCL context is checked too.  Every frame must be bit-identical
+to a one-device frame, with the same ray counts."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _frame(rt, name, res, spp=None):
+    fr = rt.make(name).with_resolution(*res)
+    return fr.with_(spp=spp) if spp else fr
+
+
+def _single(gpu_ctx, rt, fr, flags=0):
+    gpu_ctx.set_scene(fr.scene)
+    return gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=flags))
+
+
+def _rays(st):
+    return (st.primary_rays, st.shadow_rays, st.reflection_rays)
+
+
+@pytest.mark.parametrize("devices,gather", [([0, 0], 1), ([0, 0, 0], 1), ([0] * 8, 1), ([0], 2)])
+def test_group_frame_bit_identical(gpu_ctx, rt, devices, gather):
+    ctx = rt.Context(devices=devices, gather=gather)
+    try:
+        info = ctx.device_info()
+        assert info["num_devices"] == len(devices) and info["gather"] == gather
+        for name, res, spp in (("C2", (333, 217), 4), ("C3", (480, 270), 4), ("C1", (97, 61), 1)):
+            fr = _frame(rt, name, res, spp)
+            ref, sref = _single(gpu_ctx, rt, fr)
+            ctx.set_scene(fr.scene)
+            img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+            assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), (name, devices, gather)
+            assert _rays(st) == _rays(sref), (name, devices)
+            assert st.kernel_ms > 0
+    finally:
+        ctx.close()
+
+
+def test_group_output_formats_and_device_output(gpu_ctx, rt):
+    """RGBA8 / RGB32F / RGBA16F frames and rt_render_device on a group."""
+    fr = _frame(rt, "C3", (250, 131))
+    ctx = rt.Context(devices=[0, 0, 0], gather=1)
+    try:
+        ctx.set_scene(fr.scene)
+        for flags in (rt.abi.RT_FLAG_OUT_RGBA8, rt.abi.RT_FLAG_OUT_RGB32F, rt.abi.RT_FLAG_OUT_RGBA16F):
+            ref, _ = _single(gpu_ctx, rt, fr, flags)
+            img, _ = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=flags))
+            assert np.array_equal(img.view(np.uint8), ref.view(np.uint8)), flags
+        ref, _ = _single(gpu_ctx, rt, fr)
+        dev = torch.empty((131, 250, 4), dtype=torch.float32, device="cuda")
+        st = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr), dev.data_ptr(), dev.numel() * 4)
+        assert np.array_equal(dev.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        assert st.primary_rays == 250 * 131 * fr.spp
+    finally:
+        ctx.close()
+
+
+def test_group_async_frames_on_several_streams(gpu_ctx, rt):
+    """RT_FLAG_ASYNC frames of a group on two streams of device 0 (frames in
+    flight); rt_finish sums every member's counters."""
+    fr = _frame(rt, "C2", (320, 180))
+    ref, sref = _single(gpu_ctx, rt, fr)
+    ctx = rt.Context(devices=[0, 0, 0], gather=1)
+    try:
+        ctx.set_scene(fr.scene)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = [torch.empty((180, 320, 4), dtype=torch.float32, device="cuda") for _ in streams]
+        p = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC)
+        for k in range(6):
+            ctx.set_stream(streams[k % 2].cuda_stream)
+            ctx.render_device(fr.camera, fr.plane, p, outs[k % 2].data_ptr(), outs[0].numel() * 4)
+        st = ctx.finish()
+        torch.cuda.synchronize()
+        for o in outs:
+            assert np.array_equal(o.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+        assert _rays(st) == tuple(6 * v for v in _rays(sref))
+        assert st.kernel_ms > 0
+    finally:
+        ctx.close()
+
+
+def test_group_scene_source_per_frame_update(gpu_ctx, rt):
+    """Device mesh extraction + GPU rebuild (rt_set_scene_source /
+    rt_update_mesh_transforms) on every member of a group: each animated
+    frame equals the one-device frame."""
+    fr, srcs, mats = rt.scenes.instanced_hall(400, res=(160, 90), spp=4, bounces=4)
+    ctx = rt.Context(devices=[0, 0, 0], gather=1)
+    try:
+        gpu_ctx.set_scene_source(fr.scene, srcs)
+        ctx.set_scene_source(fr.scene, srcs)
+        for k, t in enumerate((0.0, 0.6, 1.7)):
+            if k:
+                gpu_ctx.update_mesh_transforms(mats(t))
+                ctx.update_mesh_transforms(mats(t))
+            ref, sref = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+            img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+            assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), t
+            assert _rays(st) == _rays(sref), t
+    finally:
+        ctx.close()
+
+
+def test_rccl_n_devices_when_present(gpu_ctx, rt):
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("one GPU visible: the N-device RCCL context needs N GPUs (logical shards cover the path)")
+    fr = _frame(rt, "C3", (480, 270))
+    ref, sref = _single(gpu_ctx, rt, fr)
+    ctx = rt.Context(num_gpus=n)
+    try:
+        assert ctx.device_info()["gather"] == rt.abi.RT_GATHER_RCCL
+        ctx.set_scene(fr.scene)
+        img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+        assert _rays(st) == _rays(sref)
+    finally:
+        ctx.close()
+
+
+def test_group_rejects_bad_device_lists(rt):
+    for devs, gather in (([0, 0], 2), ([99], 0), ([0, 0], 7)):
+        with pytest.raises(rt.RtError):
+            rt.Context(devices=devs, gather=gather)
+
+
+def test_full_size_slabbed_host_frame_equals_device_frame(gpu_ctx, rt):
+    """rt_render's host output of a full 1080p frame (rendered in row slabs,
+    each copied while the next renders) equals rt_render_device's frame."""
+    fr = rt.make("C3")
+    gpu_ctx.set_scene(fr.scene)
+    img, st = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+    dev = torch.empty((1080, 1920, 4), dtype=torch.float32, device="cuda")
+    st2 = gpu_ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr), dev.data_ptr(), dev.numel() * 4)
+    torch.cuda.synchronize()
+    assert np.array_equal(img.view(np.uint32), dev.cpu().numpy().view(np.uint32))
+    assert _rays(st) == _rays(st2)

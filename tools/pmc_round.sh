@@ -6,8 +6,9 @@ tag=${1:-cur}
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 run() {
+  # one counter group per rocprofv3 run
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $2 --output-format csv -d $R/gpurun_out/pmc_$tag/$1 -o run -- \
-    python $R/tools/probe.py --config C3 --modes megakernel --frames 3 > $R/gpurun_out/pmc_$tag/$1.log 2>&1
+    python3 $R/tools/probe.py --config C3 --modes megakernel --frames 3 > $R/gpurun_out/pmc_$tag/$1.log 2>&1
 }
 mkdir -p $R/gpurun_out/pmc_$tag
 run A "TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B TCC_EA0_RDREQ" &&

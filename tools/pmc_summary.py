@@ -12,9 +12,12 @@ counted too, so this is an upper bound on DRAM bytes):
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(dirs):
@@ -38,6 +41,9 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--kernel", default="render_kernel<false>")
     ap.add_argument("--out", default="")
+    ap.add_argument("--lib", default=os.path.join(ROOT, "unity-raytracer_amd", "lib", "librt_mi355.so"),
+                    help="the library the counters were measured with (its sha256 is recorded; bench.py uses "
+                         "the counters only with the same build)")
     a = ap.parse_args()
     vals = load(a.dirs)
     summary = {}
@@ -57,7 +63,13 @@ def main():
             w64 = c.get("TCC_EA0_WRREQ_64B", 0.0)
             wr = 64 * w64 + 32 * (c["TCC_EA0_WRREQ"] - w64)
         res.update({"kernel": name, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-                    "hbm_bytes_per_launch": (rd or 0) + (wr or 0) if rd is not None else None})
+                    "hbm_bytes_per_launch": (rd or 0) + (wr or 0) if rd is not None else None,
+                    "counters": c})
+    if os.path.exists(a.lib):
+        h = hashlib.sha256()
+        with open(a.lib, "rb") as f:
+            h.update(f.read())
+        res["lib_sha256"] = h.hexdigest()
     print(json.dumps(res, indent=1))
     if a.out:
         json.dump(res, open(a.out, "w"), indent=1)

@@ -13,7 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "librt_mi355.so")
 
-RT_ABI_VERSION = 1
+RT_ABI_VERSION = 2
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -34,6 +34,9 @@ RT_FLAG_ROW_ORDER = 64
 RT_BUILD_SAH_HOST = 0
 RT_BUILD_LBVH_GPU = 1
 RT_BUILD_LBVH_GPU_BVH2 = 2
+RT_GATHER_NONE = 0
+RT_GATHER_PEER_COPY = 1
+RT_GATHER_RCCL = 2
 
 STATUS_NAMES = {
     RT_OK: "RT_OK",
@@ -143,10 +146,15 @@ class rt_stats(C.Structure):
         ("shading_fetches", C.c_uint64),
         ("kernel_ms", C.c_double),
         ("total_ms", C.c_double),
+        ("primary_scene_misses", C.c_uint64),
     ]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class rt_device_info(C.Structure):
+    _fields_ = [("num_devices", C.c_int32), ("gather", C.c_int32), ("devices", C.c_int32 * 16)]
 
 
 class rt_mesh_source(C.Structure):
@@ -187,6 +195,8 @@ _P = C.c_void_p
 SIGNATURES = {
     "rt_abi_version": (C.c_int32, []),
     "rt_create": (C.c_int, [C.POINTER(_P), C.c_int32]),
+    "rt_create_devices": (C.c_int, [C.POINTER(_P), _P, C.c_int32, C.c_int32]),
+    "rt_get_device_info": (C.c_int, [_P, C.POINTER(rt_device_info)]),
     "rt_destroy": (None, [_P]),
     "rt_last_error": (C.c_char_p, [_P]),
     "rt_set_stream": (C.c_int, [_P, _P]),

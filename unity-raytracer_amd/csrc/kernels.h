@@ -34,7 +34,8 @@ hipError_t launch_render_wavefront(const rtd::SceneDev &S, const rtd::FrameDev &
                                    int chunk_tiles, bool count_tests, hipStream_t stream);
 
 // Batch closest hit, Scene.IntersectRay (Scene.cs:43-122): rays are 6 floats
-// (origin, direction); out[i] = {rank or -1, distance bits, -, -}.
+// (origin, direction); out[i] = {rank or -1, distance bits, rank of the closest
+// mesh-triangle hit or -1 (the reference's stale MeshIndex), -}.
 hipError_t launch_intersect(const rtd::SceneDev &S, const float *rays, int n, int4 *out,
                             hipStream_t stream);
 

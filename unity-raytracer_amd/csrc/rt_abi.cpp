@@ -19,7 +19,12 @@
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
+#include <thread>
+
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "bvh.h"
 #include "kernels.h"
@@ -57,6 +62,7 @@ struct LbvhBufs {
 // keys, the order sorted from them, for one frame layout and scene version.
 struct LptSlot {
     hipStream_t stream = nullptr;
+    int slab = 0;  // rt_render row slab (0 for whole frames)
     bool used = false;
     GrowBuf cost, cost_sorted, iota, order, scratch;
     long long key = -1;
@@ -71,7 +77,7 @@ struct LptSlot {
         }
     }
 };
-constexpr int kLptSlots = 4;
+constexpr int kLptSlots = 16;  // streams x row slabs
 
 // State kept by rt_set_scene_source for rt_update_mesh_transforms.
 struct SourceState {
@@ -85,6 +91,57 @@ struct SourceState {
 struct DeviceArrays {
     void *nodes = nullptr, *nodes4 = nullptr, *leaves = nullptr, *tris = nullptr, *sphs = nullptr, *shade = nullptr,
          *mats = nullptr, *lights = nullptr, *gates = nullptr;
+};
+
+// Frame buffers of a multi-device context for one stream of device 0 (frames
+// in flight on different streams never share them).
+constexpr int kGroupSlots = 8;
+struct GroupSlot {
+    hipStream_t root_stream = nullptr;
+    bool used = false;
+    std::vector<hipStream_t> member_stream;  // per member (member 0: a stream of its own for the RCCL self send)
+    std::vector<hipEvent_t> member_done;     // recorded on a member's stream after its band left
+    std::vector<GrowBuf> member_out;         // per member: its band, on its device
+    GrowBuf gather;                          // device 0: every band back to back
+    hipEvent_t gather_free = nullptr;        // device 0: the last frame's bands are reassembled
+};
+
+// RCCL, resolved at run time (only a multi-device context with an RCCL gather
+// needs it; a single-GPU host never loads it).
+struct Rccl {
+    bool tried = false, ok = false;
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+Rccl &rccl() {
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    // the process's RCCL when one is loaded (PyTorch's has this soname), else ROCm's
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return r;
+    r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+    r.send = (decltype(r.send))dlsym(h, "ncclSend");
+    r.recv = (decltype(r.recv))dlsym(h, "ncclRecv");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.send && r.recv && r.error_string;
+    return r;
+}
+
+// roctx ranges around the host-side phases (visible in rocprofv3 --marker-trace).
+struct Range {
+    explicit Range(const char *name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
 };
 
 }  // namespace
@@ -107,7 +164,7 @@ struct rt_ctx {
     size_t rays_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // RT_FLAG_ASYNC frames: pending count, accumulated counters and device time
-    hipEvent_t ev_a0 = nullptr, ev_a1 = nullptr;
+    hipEvent_t ev_a0 = nullptr;
     int async_frames = 0;
     long long async_total_frames = 0;
     unsigned long long async_acc[rtd::kCounterWords] = {0};
@@ -129,6 +186,18 @@ struct rt_ctx {
     LptSlot lpt[kLptSlots];
     unsigned long long scene_version = 0;
     SourceState src;
+    // end event of the last RT_FLAG_ASYNC frame per stream: rt_finish's device
+    // time spans from the first async frame to the last of them to finish
+    std::vector<std::pair<hipStream_t, hipEvent_t>> async_end;
+    // rt_render's slab pipeline: copy stream + one event per slab
+    hipStream_t copy_stream = nullptr;
+    std::vector<hipEvent_t> slab_done;
+    // multi-device context: this context is member 0 (the root, device 0 of
+    // the frame); peers[i] is member i + 1, a single-device context of its own
+    std::vector<rt_ctx *> peers;
+    int gather = RT_GATHER_NONE;
+    std::vector<ncclComm_t> comms;  // one per member (RT_GATHER_RCCL)
+    GroupSlot gslots[kGroupSlots];
 };
 
 namespace {
@@ -311,6 +380,20 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     return RT_OK;
 }
 
+// The context's own device output buffer (rt_render), grow-only.
+hipError_t ensure_out(rt_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->d_out_cap) return hipSuccess;
+    if (ctx->d_out) {
+        hipError_t e = hipFree(ctx->d_out);
+        if (e != hipSuccess) return e;
+    }
+    ctx->d_out = nullptr;
+    ctx->d_out_cap = 0;
+    hipError_t e = hipMalloc(&ctx->d_out, bytes);
+    if (e == hipSuccess) ctx->d_out_cap = bytes;
+    return e;
+}
+
 // Upper bound on wavefront pool entries (64 B each) per chunk: 160M = 10 GB.
 constexpr size_t kPoolBudget = (size_t)160 << 20;
 constexpr size_t kShadowBudget = (size_t)96 << 20;
@@ -419,6 +502,9 @@ constexpr int kSplit16DivLarge = RT_SPLIT16_DIV_LARGE;
 #define RT_LPT_PERIOD 16
 #endif
 constexpr int kLptPeriod = RT_LPT_PERIOD;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
+// rt_render's host-output pipeline: about this many bytes per row slab, at most kMaxSlabs slabs
+constexpr size_t kSlabBytes = (size_t)6 << 20;
+constexpr int kMaxSlabs = 8;
 
 // Sums the sharded ray/test counters on the host (the stream must be idle).
 int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
@@ -440,6 +526,7 @@ void fill_stats(rt_stats *stats, const unsigned long long counts[rtd::kCounterWo
     stats->triangle_tests = counts[4];
     stats->sphere_tests = counts[5];
     stats->shading_fetches = counts[6];
+    stats->primary_scene_misses = counts[7];
     stats->kernel_ms = kernel_ms;
     stats->total_ms = total_ms;
 }
@@ -454,21 +541,143 @@ int settle_async(rt_ctx *ctx) {
     int st = read_counters(ctx, counts);
     if (st) return st;
     for (int w = 0; w < rtd::kCounterWords; ++w) ctx->async_acc[w] += counts[w];
+    // the frames since ev_a0 may have run on several streams: their device
+    // time ends with the last of the streams' final frames
     float ms = 0.0f;
-    HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev_a0, ctx->ev_a1));
+    for (auto &se : ctx->async_end) {
+        if (!se.first) continue;
+        float m = 0.0f;
+        HIP_OR_FAIL(ctx, hipEventElapsedTime(&m, ctx->ev_a0, se.second));
+        ms = std::max(ms, m);
+        se.first = nullptr;  // the event object is kept for reuse
+    }
     ctx->async_ms += ms;
     ctx->async_frames = 0;
     return RT_OK;
 }
 
+// Records the end of an RT_FLAG_ASYNC frame on the context's current stream.
+int record_async_end(rt_ctx *ctx) {
+    hipEvent_t ev = nullptr;
+    for (auto &se : ctx->async_end)
+        if (se.first == ctx->stream) ev = se.second;
+    if (!ev) {
+        for (auto &se : ctx->async_end)
+            if (!se.first && !ev) {
+                se.first = ctx->stream;
+                ev = se.second;
+            }
+    }
+    if (!ev) {
+        HIP_OR_FAIL(ctx, hipEventCreate(&ev));
+        ctx->async_end.emplace_back(ctx->stream, ev);
+    }
+    HIP_OR_FAIL(ctx, hipEventRecord(ev, ctx->stream));
+    return RT_OK;
+}
+
+// Longest-first dispatch of a megakernel launch: picks the state of
+// (stream, slab), points F at the last measured order and decides whether
+// this launch measures costs (the caller sorts them after the launch).
+int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool mega, bool count, int slab,
+                LptSlot *&ls, bool &lpt_sort) {
+    ls = nullptr;
+    lpt_sort = false;
+    F.tile_order = nullptr;
+    F.tile_cost = nullptr;
+    if (!mega || (prm->flags & RT_FLAG_ROW_ORDER) != 0 || F.num_tiles <= 0) return RT_OK;
+    for (LptSlot &l : ctx->lpt)
+        if (l.used && l.stream == ctx->stream && l.slab == slab) ls = &l;
+    if (!ls)
+        for (LptSlot &l : ctx->lpt)
+            if (!l.used && !ls) {
+                ls = &l;
+                ls->used = true;
+                ls->stream = ctx->stream;
+                ls->slab = slab;
+            }
+    if (!ls) return RT_OK;  // more (stream, slab) pairs than slots: row-major order
+    const long long key = ((long long)F.num_tiles << 32) ^ ((long long)F.tiles_x << 20) ^ ((long long)F.spp << 12) ^
+                          ((long long)F.band_count << 6) ^ F.band_index ^ ((long long)F.row0 << 44);
+    if (key != ls->key) {
+        const size_t n = (size_t)F.num_tiles;
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->cost, n * 4));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->cost_sorted, n * 4));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->order, n * 4));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->scratch, rtk::tile_sort_scratch_bytes(F.num_tiles)));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->iota, n * 4));
+        HIP_OR_FAIL(ctx, rtk::launch_iota((int *)ls->iota.p, F.num_tiles, ctx->stream));
+        ls->key = key;
+        ls->valid = false;
+    }
+    if (ls->scene != ctx->scene_version) {
+        ls->scene = ctx->scene_version;
+        ls->valid = false;
+    }
+    if (!ls->valid) ls->frames = 0;
+    F.tile_order = ls->valid ? (const int *)ls->order.p : nullptr;
+    // costs are measured and re-sorted every kLptPeriod frames (the sort
+    // costs more than a small frame's tail)
+    lpt_sort = !ls->valid || ls->frames % kLptPeriod == 0;
+    F.tile_cost = lpt_sort ? (unsigned *)ls->cost.p : nullptr;
+    ++ls->frames;
+    // the most expensive tiles of the last measurement are split into
+    // quarter-waves (a frame's time is bounded below by its slowest wave);
+    // render_kernel only: 16 lanes must hold whole pixels
+    const bool levels = ctx->S.bvh4 && F.spp >= 16;
+    if (F.tile_order && !count && !levels && kSplitDiv > 0 && 16 % F.spp == 0 && F.num_tiles <= kSplitMaxTiles) {
+        F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
+        // sixteenth-waves (4 lanes) must hold whole pixels too
+        if (kSplit16Div > 0 && 4 % F.spp == 0) {
+            F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / kSplit16Div));
+            F.split_tiles -= F.split16_tiles;
+        }
+    } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
+               F.num_tiles <= kSplit16MaxTiles) {
+        F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
+    }
+    return RT_OK;
+}
+
+int lpt_sort_now(rt_ctx *ctx, const rtd::FrameDev &F, LptSlot *ls) {
+    HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
+                                             (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles, ls->scratch.p,
+                                             ls->scratch.cap, ctx->stream));
+    ls->valid = true;
+    return RT_OK;
+}
+
+// The render path a frame takes.
+struct Path {
+    bool count, packet, wavefront, mega;
+};
+
+Path frame_path(const rt_ctx *ctx, const rt_render_params *prm) {
+    Path p;
+    p.count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
+    p.packet = (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
+    p.wavefront = !p.packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
+    p.mega = !p.packet && !p.wavefront;  // default
+    return p;
+}
+
+// Enqueues the trace launch(es) of F on the context's stream.
+int launch_frame(rt_ctx *ctx, rtd::FrameDev &F, const Path &P, const rtw::Args &A, int chunk_tiles) {
+    if (P.packet)
+        HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, P.count, ctx->stream));
+    else if (P.mega)
+        HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, P.count, ctx->stream));
+    else if (P.wavefront && F.num_tiles > 0)
+        HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, P.count, ctx->stream));
+    return RT_OK;
+}
+
 int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *d_out, rt_stats *stats,
               std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes) {
+    Range range("rt_frame");
     F.out = d_out;
     F.counters = ctx->d_counters;
-    const bool count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
-    const bool packet = (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
-    const bool wavefront = !packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
-    const bool mega = !packet && !wavefront;  // default
+    const Path P = frame_path(ctx, prm);
     const bool async = (prm->flags & RT_FLAG_ASYNC) != 0;
     if (async && host_out) return fail(ctx, RT_E_INVALID, "RT_FLAG_ASYNC needs a device output (rt_render_device)");
     if (!async) {
@@ -477,7 +686,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     }
     int chunk_tiles = 0;
     rtw::Args A{};
-    if (wavefront && F.num_tiles > 0) {
+    if (P.wavefront && F.num_tiles > 0) {
         int st = prepare_wavefront(ctx, F, chunk_tiles, A);
         if (st) return st;
     }
@@ -491,94 +700,88 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         // frames): it must not count before the counters were zeroed
         HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_a0, 0));
     }
-    // megakernel frames dispatch a previous frame's most expensive tiles
-    // first (a frame's tail is its slowest tiles); the order is kept per stream
-    LptSlot *ls = nullptr;
-    bool lpt_sort = false;
-    F.tile_order = nullptr;
-    F.tile_cost = nullptr;
-    if (mega && (prm->flags & RT_FLAG_ROW_ORDER) == 0 && F.num_tiles > 0) {
-        for (LptSlot &l : ctx->lpt)
-            if (l.used && l.stream == ctx->stream) ls = &l;
-        if (!ls)
-            for (LptSlot &l : ctx->lpt)
-                if (!l.used && !ls) {
-                    ls = &l;
-                    ls->used = true;
-                    ls->stream = ctx->stream;
-                }
-    }
-    if (ls) {  // (more than kLptSlots streams: the extra ones keep row-major order)
-        const long long key = ((long long)F.num_tiles << 32) ^ ((long long)F.tiles_x << 20) ^
-                              ((long long)F.spp << 12) ^ ((long long)F.band_count << 6) ^ F.band_index;
-        if (key != ls->key) {
-            const size_t n = (size_t)F.num_tiles;
-            HIP_OR_FAIL(ctx, ensure(ctx, ls->cost, n * 4));
-            HIP_OR_FAIL(ctx, ensure(ctx, ls->cost_sorted, n * 4));
-            HIP_OR_FAIL(ctx, ensure(ctx, ls->order, n * 4));
-            HIP_OR_FAIL(ctx, ensure(ctx, ls->scratch, rtk::tile_sort_scratch_bytes(F.num_tiles)));
-            HIP_OR_FAIL(ctx, ensure(ctx, ls->iota, n * 4));
-            HIP_OR_FAIL(ctx, rtk::launch_iota((int *)ls->iota.p, F.num_tiles, ctx->stream));
-            ls->key = key;
-            ls->valid = false;
+    // rt_render into a host Color[]: the frame in row slabs, each copied to the
+    // host while the next ones render (the PCIe copy is the longer part)
+    const bool slabs = host_out && out_bytes && F.band_count == 1 && !P.wavefront;
+    if (slabs) {
+        const int row_bytes = (int)(out_bytes / (size_t)std::max(1, F.local_rows));
+        const int nslab = std::max(1, std::min(kMaxSlabs, (int)(out_bytes / kSlabBytes)));
+        // slab boundaries on whole tile rows
+        const int tile_rows = (F.local_rows + F.tile_h - 1) / F.tile_h;
+        if (!ctx->copy_stream) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+        while ((int)ctx->slab_done.size() < nslab) {
+            hipEvent_t e;
+            HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ctx->slab_done.push_back(e);
         }
-        if (ls->scene != ctx->scene_version) {
-            ls->scene = ctx->scene_version;
-            ls->valid = false;
+        const rtd::FrameDev F0 = F;
+        std::vector<std::pair<LptSlot *, rtd::FrameDev>> sorts;
+        std::vector<std::pair<int, int>> bounds;
+        for (int k = 0; k < nslab; ++k) {
+            const int r0 = std::min(F0.local_rows, (int)((long long)tile_rows * k / nslab) * F0.tile_h);
+            const int r1 = std::min(F0.local_rows, (int)((long long)tile_rows * (k + 1) / nslab) * F0.tile_h);
+            rtd::FrameDev Fk = F0;
+            Fk.row0 = r0;
+            Fk.local_rows = r1 - r0;
+            Fk.num_tiles = Fk.res_x > 0 ? Fk.tiles_x * ((Fk.local_rows + Fk.tile_h - 1) / Fk.tile_h) : 0;
+            Fk.out = (char *)d_out + (size_t)r0 * row_bytes;
+            LptSlot *ls = nullptr;
+            bool lpt_sort = false;
+            int st = lpt_prepare(ctx, Fk, prm, P.mega, P.count, k, ls, lpt_sort);
+            if (st) return st;
+            st = launch_frame(ctx, Fk, P, A, chunk_tiles);
+            if (st) return st;
+            HIP_OR_FAIL(ctx, hipEventRecord(ctx->slab_done[k], ctx->stream));
+            if (lpt_sort) sorts.emplace_back(ls, Fk);
+            bounds.emplace_back(r0, r1);
         }
-        if (!ls->valid) ls->frames = 0;
-        F.tile_order = ls->valid ? (const int *)ls->order.p : nullptr;
-        // costs are measured and re-sorted every kLptPeriod frames (the sort
-        // costs more than a small frame's tail)
-        lpt_sort = !ls->valid || ls->frames % kLptPeriod == 0;
-        F.tile_cost = lpt_sort ? (unsigned *)ls->cost.p : nullptr;
-        ++ls->frames;
-        // the most expensive tiles of the last measurement are split into
-        // quarter-waves (a frame's time is bounded below by its slowest
-        // wave); render_kernel only: 16 lanes must hold whole pixels
-        const bool levels = ctx->S.bvh4 && F.spp >= 16;
-        if (F.tile_order && !count && !levels && kSplitDiv > 0 && 16 % F.spp == 0 && F.num_tiles <= kSplitMaxTiles) {
-            F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
-            // sixteenth-waves (4 lanes) must hold whole pixels too
-            if (kSplit16Div > 0 && 4 % F.spp == 0) {
-                F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / kSplit16Div));
-                F.split_tiles -= F.split16_tiles;
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+        for (auto &so : sorts) {  // after the timed region: the order of the next frames
+            int st = lpt_sort_now(ctx, so.second, so.first);
+            if (st) return st;
+        }
+        // every launch is enqueued before the first copy: a copy into pageable
+        // memory may hold the host until it is done
+        for (int k = 0; k < nslab; ++k) {
+            const int r0 = bounds[k].first, r1 = bounds[k].second;
+            if (r1 <= r0) continue;
+            HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->copy_stream, ctx->slab_done[k], 0));
+            HIP_OR_FAIL(ctx, hipMemcpyAsync((char *)host_out + (size_t)r0 * row_bytes,
+                                            (const char *)d_out + (size_t)r0 * row_bytes,
+                                            (size_t)(r1 - r0) * row_bytes, hipMemcpyDeviceToHost, ctx->copy_stream));
+        }
+        HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->copy_stream));
+    } else {
+        // megakernel frames dispatch a previous frame's most expensive tiles
+        // first (a frame's tail is its slowest tiles); the order is kept per stream
+        LptSlot *ls = nullptr;
+        bool lpt_sort = false;
+        int st = lpt_prepare(ctx, F, prm, P.mega, P.count, 0, ls, lpt_sort);
+        if (st) return st;
+        st = launch_frame(ctx, F, P, A, chunk_tiles);
+        if (st) return st;
+        if (async) {
+            if (lpt_sort) {
+                st = lpt_sort_now(ctx, F, ls);
+                if (st) return st;
             }
-        } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
-                   F.num_tiles <= kSplit16MaxTiles) {
-            F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
+            st = record_async_end(ctx);
+            if (st) return st;
+            if (ctx->async_frames++ == 0 && ctx->async_t0_set == false) {
+                ctx->async_t0 = t_start;
+                ctx->async_t0_set = true;
+            }
+            if (stats) std::memset(stats, 0, sizeof *stats);
+            return RT_OK;
         }
-    }
-    if (packet)
-        HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, count, ctx->stream));
-    else if (mega)
-        HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, count, ctx->stream));
-    else if (wavefront && F.num_tiles > 0)
-        HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, count, ctx->stream));
-    if (async) {
-        if (lpt_sort) {
-            HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
-                                                     (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
-                                                     ls->scratch.p, ls->scratch.cap, ctx->stream));
-            ls->valid = true;
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+        if (lpt_sort) {  // after the timed region: the order of the next frames
+            st = lpt_sort_now(ctx, F, ls);
+            if (st) return st;
         }
-        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_a1, ctx->stream));
-        if (ctx->async_frames++ == 0 && ctx->async_t0_set == false) {
-            ctx->async_t0 = t_start;
-            ctx->async_t0_set = true;
-        }
-        if (stats) std::memset(stats, 0, sizeof *stats);
-        return RT_OK;
+        if (host_out && out_bytes)
+            HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     }
-    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    if (lpt_sort) {  // after the timed region: the order of the next frames
-        HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
-                                                 (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
-                                                 ls->scratch.p, ls->scratch.cap, ctx->stream));
-        ls->valid = true;
-    }
-    if (host_out && out_bytes)
-        HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     unsigned long long counts[rtd::kCounterWords];
     int st = read_counters(ctx, counts);
@@ -763,17 +966,14 @@ int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
 
 float rt_spec_threshold(void) { return spec_threshold(); }
 
-int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
-    if (!out_ctx) return fail(nullptr, RT_E_INVALID, "out_ctx is null");
-    *out_ctx = nullptr;
-    if (num_gpus != 1)
-        return fail(nullptr, RT_E_INVALID,
-                    "num_gpus must be 1: one context per GPU; shard rows with band_index/band_count");
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
-        return fail(nullptr, RT_E_NO_DEVICE, "no HIP device visible");
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return fail(nullptr, RT_E_NO_DEVICE, "hipGetDevice failed");
+}  // extern "C"
+
+namespace {
+
+// A single-device context on device `dev` (made current).
+int create_one(int dev, rt_ctx **out) {
+    *out = nullptr;
+    if (hipSetDevice(dev) != hipSuccess) return fail(nullptr, RT_E_NO_DEVICE, "hipSetDevice(%d) failed", dev);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
         return fail(nullptr, RT_E_NO_DEVICE, "hipGetDeviceProperties failed");
@@ -784,22 +984,21 @@ int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev_a0) != hipSuccess || hipEventCreate(&c->ev_a1) != hipSuccess ||
-        hipMalloc(&c->d_counters,
-                  rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long)) !=
+        hipEventCreate(&c->ev_a0) != hipSuccess ||
+        hipMalloc(&c->d_counters, rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long)) !=
             hipSuccess) {
         rt_destroy(c);
         return fail(nullptr, RT_E_HIP, "stream/event/counter allocation failed");
     }
     c->stream = c->own_stream;
-    *out_ctx = c;
+    *out = c;
     return RT_OK;
 }
 
-void rt_destroy(rt_ctx *ctx) {
-    if (!ctx) return;
+void destroy_one(rt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
     free_scene(ctx);
     free_wavefront(ctx);
     ctx->lb.release();
@@ -811,10 +1010,376 @@ void rt_destroy(rt_ctx *ctx) {
     if (ctx->d_hits) (void)hipFree(ctx->d_hits);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev_a0) (void)hipEventDestroy(ctx->ev_a0);
-    if (ctx->ev_a1) (void)hipEventDestroy(ctx->ev_a1);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    for (auto &se : ctx->async_end) (void)hipEventDestroy(se.second);
+    for (hipEvent_t e : ctx->slab_done) (void)hipEventDestroy(e);
+    if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
+}
+
+int nmembers(const rt_ctx *c) { return 1 + (int)c->peers.size(); }
+rt_ctx *member(rt_ctx *c, int i) { return i == 0 ? c : c->peers[(size_t)i - 1]; }
+
+// The library switches devices; the caller's current device is restored on return.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
+// fn(member) for every member of a context, each on a host thread of its own
+// when there are several (the host BVH build of a scene runs on every device
+// at once); the first failure is reported on ctx.
+template <typename Fn>
+int for_members(rt_ctx *ctx, Fn fn) {
+    const int n = nmembers(ctx);
+    if (n == 1) return fn(ctx);
+    std::vector<int> st((size_t)n, RT_OK);
+    std::vector<std::thread> th;
+    th.reserve((size_t)n);
+    for (int i = 0; i < n; ++i) th.emplace_back([&, i] { st[(size_t)i] = fn(member(ctx, i)); });
+    for (auto &t : th) t.join();
+    for (int i = 0; i < n; ++i)
+        if (st[(size_t)i] != RT_OK) {
+            if (i) ctx->err = "device " + std::to_string(member(ctx, i)->device) + ": " + member(ctx, i)->err;
+            return st[(size_t)i];
+        }
+    return RT_OK;
+}
+
+void release_group(rt_ctx *ctx) {
+    Rccl &R = rccl();
+    for (ncclComm_t c : ctx->comms)
+        if (c && R.ok) (void)R.comm_destroy(c);
+    ctx->comms.clear();
+    const int n = nmembers(ctx);
+    for (GroupSlot &g : ctx->gslots) {
+        if (!g.used) continue;
+        for (int i = 0; i < n && i < (int)g.member_stream.size(); ++i) {
+            (void)hipSetDevice(member(ctx, i)->device);
+            if (g.member_stream[(size_t)i]) {
+                (void)hipStreamSynchronize(g.member_stream[(size_t)i]);
+                (void)hipStreamDestroy(g.member_stream[(size_t)i]);
+            }
+            if (g.member_done[(size_t)i]) (void)hipEventDestroy(g.member_done[(size_t)i]);
+            if (g.member_out[(size_t)i].p) (void)hipFree(g.member_out[(size_t)i].p);
+        }
+        (void)hipSetDevice(ctx->device);
+        if (g.gather.p) (void)hipFree(g.gather.p);
+        if (g.gather_free) (void)hipEventDestroy(g.gather_free);
+        g = GroupSlot{};
+    }
+    for (rt_ctx *p : ctx->peers) destroy_one(p);
+    ctx->peers.clear();
+}
+
+// A context over `devices` (devices[0] = root; repeats = logical shards).
+int create_group(const int32_t *devices, int32_t n, int32_t gather, rt_ctx **out_ctx) {
+    DeviceGuard guard;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(nullptr, RT_E_NO_DEVICE, "no HIP device visible");
+    bool distinct = true;
+    for (int i = 0; i < n; ++i) {
+        if (devices[i] < 0 || devices[i] >= count)
+            return fail(nullptr, RT_E_NO_DEVICE, "device %d not visible (%d devices)", devices[i], count);
+        for (int j = 0; j < i; ++j)
+            if (devices[j] == devices[i]) distinct = false;
+    }
+    if (gather == 0) gather = n > 1 ? (distinct ? RT_GATHER_RCCL : RT_GATHER_PEER_COPY) : RT_GATHER_NONE;
+    if (gather == RT_GATHER_NONE && n > 1)
+        return fail(nullptr, RT_E_INVALID, "a %d-device context needs a gather transport", n);
+    if (gather == RT_GATHER_RCCL && !distinct)
+        return fail(nullptr, RT_E_INVALID, "RT_GATHER_RCCL needs distinct devices (one RCCL rank per GPU)");
+    if (gather != RT_GATHER_NONE && gather != RT_GATHER_PEER_COPY && gather != RT_GATHER_RCCL)
+        return fail(nullptr, RT_E_INVALID, "unknown gather transport %d", gather);
+    rt_ctx *root = nullptr;
+    int st = create_one(devices[0], &root);
+    if (st) return st;
+    for (int i = 1; i < n; ++i) {
+        rt_ctx *p = nullptr;
+        st = create_one(devices[i], &p);
+        if (st) {
+            release_group(root);
+            destroy_one(root);
+            return st;
+        }
+        root->peers.push_back(p);
+    }
+    root->gather = gather;
+    if (gather == RT_GATHER_PEER_COPY && distinct) {
+        // direct xGMI copies between the root and every other device
+        for (int i = 1; i < n; ++i) {
+            (void)hipSetDevice(devices[0]);
+            hipError_t e = hipDeviceEnablePeerAccess(devices[i], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+            (void)hipSetDevice(devices[i]);
+            e = hipDeviceEnablePeerAccess(devices[0], 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        }
+    }
+    if (gather == RT_GATHER_RCCL) {
+        Rccl &R = rccl();
+        if (!R.ok) {
+            release_group(root);
+            destroy_one(root);
+            return fail(nullptr, RT_E_NO_DEVICE, "RT_GATHER_RCCL: librccl.so.1 not loadable");
+        }
+        root->comms.assign((size_t)n, nullptr);
+        const ncclResult_t r = R.comm_init_all(root->comms.data(), n, devices);
+        if (r != ncclSuccess) {
+            root->comms.clear();
+            release_group(root);
+            destroy_one(root);
+            return fail(nullptr, RT_E_HIP, "ncclCommInitAll(%d devices): %s", n, R.error_string(r));
+        }
+    }
+    *out_ctx = root;
+    return RT_OK;
+}
+
+// The frame buffers of the root stream the next multi-device frame runs on.
+int group_slot(rt_ctx *ctx, GroupSlot *&gs) {
+    gs = nullptr;
+    for (GroupSlot &g : ctx->gslots)
+        if (g.used && g.root_stream == ctx->stream) gs = &g;
+    if (gs) return RT_OK;
+    for (GroupSlot &g : ctx->gslots)
+        if (!g.used && !gs) gs = &g;
+    if (!gs) return fail(ctx, RT_E_STATE, "more than %d streams in flight on a multi-device context", kGroupSlots);
+    const int n = nmembers(ctx);
+    gs->used = true;
+    gs->root_stream = ctx->stream;
+    gs->member_stream.assign((size_t)n, nullptr);
+    gs->member_done.assign((size_t)n, nullptr);
+    gs->member_out.assign((size_t)n, GrowBuf{});
+    for (int i = 0; i < n; ++i) {
+        HIP_OR_FAIL(ctx, hipSetDevice(member(ctx, i)->device));
+        HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&gs->member_stream[(size_t)i], hipStreamNonBlocking));
+        HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&gs->member_done[(size_t)i], hipEventDisableTiming));
+    }
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&gs->gather_free, hipEventDisableTiming));
+    return RT_OK;
+}
+
+// A member's RT_FLAG_ASYNC bookkeeping, set aside while a synchronous
+// multi-device frame uses it (so that frame's stats are its own).
+struct AsyncStash {
+    unsigned long long acc[rtd::kCounterWords];
+    double ms;
+    bool t0_set;
+    std::chrono::steady_clock::time_point t0;
+};
+
+void stash_async(rt_ctx *m, AsyncStash &s) {
+    std::memcpy(s.acc, m->async_acc, sizeof s.acc);
+    s.ms = m->async_ms;
+    s.t0_set = m->async_t0_set;
+    s.t0 = m->async_t0;
+    std::memset(m->async_acc, 0, sizeof m->async_acc);
+    m->async_ms = 0.0;
+    m->async_t0_set = false;
+}
+
+void unstash_async(rt_ctx *m, const AsyncStash &s) {
+    std::memcpy(m->async_acc, s.acc, sizeof s.acc);
+    m->async_ms = s.ms;
+    m->async_t0_set = s.t0_set;
+    m->async_t0 = s.t0;
+}
+
+// Waits for a member's async frames and takes their counters and device time.
+int take_async(rt_ctx *m, unsigned long long counts[rtd::kCounterWords], double &ms) {
+    HIP_OR_FAIL(m, hipSetDevice(m->device));
+    const int st = settle_async(m);
+    if (st) return st;
+    std::memcpy(counts, m->async_acc, sizeof m->async_acc);
+    ms = m->async_ms;
+    std::memset(m->async_acc, 0, sizeof m->async_acc);
+    m->async_ms = 0.0;
+    m->async_t0_set = false;
+    return RT_OK;
+}
+
+// One frame on a multi-device context: member i renders row band i of N
+// (block-cyclic, 8-row blocks) on a stream of its own, the bands travel to
+// the root (RCCL send/recv in one group, or peer copies), the root puts them
+// back in row order (assemble kernel) into d_out and, with host_out, copies
+// the frame to the host.  SURVEY §8(e); RayTracingSetup.cs:288-301.
+int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, const rt_render_params *prm,
+                void *d_out, void *host_out, size_t full_bytes, rt_stats *stats,
+                std::chrono::steady_clock::time_point t0) {
+    Range range("rt_group_frame");
+    DeviceGuard guard;
+    const int n = nmembers(ctx);
+    const bool async = (prm->flags & RT_FLAG_ASYNC) != 0;
+    const int R = prm->band_rows > 0 ? prm->band_rows : 8;
+    const int px_bytes = rt_pixel_bytes(prm->flags);
+    std::vector<rtd::FrameDev> F((size_t)n);
+    std::vector<rt_render_params> mp((size_t)n, *prm);
+    size_t shard = 0;
+    for (int i = 0; i < n; ++i) {
+        mp[(size_t)i].band_index = i;
+        mp[(size_t)i].band_count = n;
+        mp[(size_t)i].band_rows = R;
+        mp[(size_t)i].flags |= RT_FLAG_ASYNC;
+        size_t b = 0;
+        int st = prepare_frame(member(ctx, i), cam, plane, &mp[(size_t)i], F[(size_t)i], b);
+        if (st) {
+            if (i) ctx->err = member(ctx, i)->err;
+            return st;
+        }
+        shard = std::max(shard, b);  // every band has local_rows rows (the last ones padded)
+    }
+    GroupSlot *gs = nullptr;
+    int st = group_slot(ctx, gs);
+    if (st) return st;
+    std::vector<AsyncStash> stash((size_t)n);
+    const bool rccl_gather = ctx->gather == RT_GATHER_RCCL;
+    // the root's band goes straight into the gather buffer unless it travels
+    // through RCCL itself (a one-device RCCL context: self send/receive)
+    const bool root_self_send = rccl_gather && n == 1;
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    HIP_OR_FAIL(ctx, ensure(ctx, gs->gather, (size_t)n * shard));
+    for (int i = 0; i < n; ++i) {
+        rt_ctx *m = member(ctx, i);
+        HIP_OR_FAIL(ctx, hipSetDevice(m->device));
+        if (!async) {
+            st = settle_async(m);  // the caller's pending async frames keep their stats
+            if (st) return st;
+            stash_async(m, stash[(size_t)i]);
+        }
+        void *out;
+        if (i == 0 && !root_self_send) {
+            out = gs->gather.p;
+        } else {
+            HIP_OR_FAIL(ctx, ensure(m, gs->member_out[(size_t)i], shard));
+            out = gs->member_out[(size_t)i].p;
+        }
+        if (i > 0) {
+            m->stream = gs->member_stream[(size_t)i];
+            // this band's slot in the gather buffer is free once the previous
+            // frame of this root stream has been reassembled
+            HIP_OR_FAIL(ctx, hipStreamWaitEvent(m->stream, gs->gather_free, 0));
+        }
+        st = run_frame(m, F[(size_t)i], &mp[(size_t)i], out, nullptr, t0, nullptr, 0);
+        if (st) {
+            if (i) ctx->err = m->err;
+            return st;
+        }
+    }
+    // gather the bands to the root
+    if (rccl_gather) {
+        Range rr("rt_gather_rccl");
+        Rccl &Rc = rccl();
+        ncclResult_t r = Rc.group_start();
+        for (int i = 1; i < n && r == ncclSuccess; ++i)
+            r = Rc.recv((char *)gs->gather.p + (size_t)i * shard, shard, ncclChar, i, ctx->comms[0], ctx->stream);
+        for (int i = 1; i < n && r == ncclSuccess; ++i)
+            r = Rc.send(gs->member_out[(size_t)i].p, shard, ncclChar, 0, ctx->comms[(size_t)i],
+                        gs->member_stream[(size_t)i]);
+        if (root_self_send && r == ncclSuccess) {
+            r = Rc.send(gs->member_out[0].p, shard, ncclChar, 0, ctx->comms[0], ctx->stream);
+            if (r == ncclSuccess) r = Rc.recv(gs->gather.p, shard, ncclChar, 0, ctx->comms[0], ctx->stream);
+        }
+        const ncclResult_t r2 = Rc.group_end();
+        if (r != ncclSuccess || r2 != ncclSuccess)
+            return fail(ctx, RT_E_HIP, "RCCL band gather: %s", Rc.error_string(r != ncclSuccess ? r : r2));
+    } else {
+        Range rr("rt_gather_peer");
+        for (int i = 1; i < n; ++i) {
+            rt_ctx *m = member(ctx, i);
+            HIP_OR_FAIL(ctx, hipSetDevice(m->device));
+            HIP_OR_FAIL(ctx, hipMemcpyPeerAsync((char *)gs->gather.p + (size_t)i * shard, ctx->device,
+                                                gs->member_out[(size_t)i].p, m->device, shard, m->stream));
+            HIP_OR_FAIL(ctx, hipEventRecord(gs->member_done[(size_t)i], m->stream));
+        }
+        HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+        for (int i = 1; i < n; ++i) HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->stream, gs->member_done[(size_t)i], 0));
+    }
+    // back to row order on the root, then (rt_render) to the host
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    const int local = F[0].local_rows;
+    HIP_OR_FAIL(ctx, rtk::launch_assemble(gs->gather.p, plane->resolution_x, plane->resolution_y, n, R, local,
+                                          px_bytes, d_out, ctx->stream));
+    HIP_OR_FAIL(ctx, hipEventRecord(gs->gather_free, ctx->stream));
+    if (host_out && full_bytes)
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, full_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if (async) {
+        if (stats) std::memset(stats, 0, sizeof *stats);
+        return RT_OK;
+    }
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long sum[rtd::kCounterWords] = {0};
+    double kms = 0.0;
+    for (int i = 0; i < n; ++i) {
+        rt_ctx *m = member(ctx, i);
+        unsigned long long c[rtd::kCounterWords];
+        double ms = 0.0;
+        st = take_async(m, c, ms);
+        unstash_async(m, stash[(size_t)i]);
+        if (st) {
+            if (i) ctx->err = m->err;
+            return st;
+        }
+        for (int w = 0; w < rtd::kCounterWords; ++w) sum[w] += c[w];
+        kms = std::max(kms, ms);
+    }
+    if (stats)
+        fill_stats(stats, sum, kms,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
+    if (!out_ctx) return fail(nullptr, RT_E_INVALID, "out_ctx is null");
+    *out_ctx = nullptr;
+    if (num_gpus < 1) return fail(nullptr, RT_E_INVALID, "num_gpus must be >= 1, got %d", num_gpus);
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(nullptr, RT_E_NO_DEVICE, "no HIP device visible");
+    if (num_gpus == 1) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return fail(nullptr, RT_E_NO_DEVICE, "hipGetDevice failed");
+        return create_one(dev, out_ctx);
+    }
+    if (num_gpus > count)
+        return fail(nullptr, RT_E_NO_DEVICE, "num_gpus %d > %d visible devices", num_gpus, count);
+    std::vector<int32_t> devs((size_t)num_gpus);
+    for (int i = 0; i < num_gpus; ++i) devs[(size_t)i] = i;
+    return create_group(devs.data(), num_gpus, 0, out_ctx);
+}
+
+int rt_create_devices(rt_ctx **out_ctx, const int32_t *devices, int32_t num_devices, int32_t gather) {
+    if (!out_ctx) return fail(nullptr, RT_E_INVALID, "out_ctx is null");
+    *out_ctx = nullptr;
+    if (num_devices < 1 || !devices) return fail(nullptr, RT_E_INVALID, "need at least one device");
+    return create_group(devices, num_devices, gather, out_ctx);
+}
+
+int rt_get_device_info(const rt_ctx *ctx, rt_device_info *info) {
+    if (!ctx || !info) return RT_E_INVALID;
+    std::memset(info, 0, sizeof *info);
+    info->num_devices = 1 + (int)ctx->peers.size();
+    info->gather = ctx->gather;
+    for (int i = 0; i < info->num_devices && i < 16; ++i)
+        info->devices[i] = i == 0 ? ctx->device : ctx->peers[(size_t)i - 1]->device;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx *ctx) {
+    if (!ctx) return;
+    DeviceGuard guard;
+    release_group(ctx);
+    destroy_one(ctx);
 }
 
 const char *rt_last_error(const rt_ctx *ctx) {
@@ -832,8 +1397,13 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) { return rt_set_scene_ex(
 
 int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
     if (!ctx) return RT_E_INVALID;
-    ctx->src.active = false;
-    return set_scene_impl(ctx, sc, build, false, std::chrono::steady_clock::now());
+    Range range("rt_set_scene");
+    DeviceGuard guard;
+    const auto t0 = std::chrono::steady_clock::now();
+    return for_members(ctx, [&](rt_ctx *m) {
+        m->src.active = false;
+        return set_scene_impl(m, sc, build, false, t0);
+    });
 }
 
 }  // extern "C"
@@ -1063,9 +1633,12 @@ int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geo
 
 extern "C" {
 
-int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count) {
-    if (!ctx) return RT_E_INVALID;
-    const auto t0 = std::chrono::steady_clock::now();
+}  // extern "C"
+
+namespace {
+
+int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count,
+                         std::chrono::steady_clock::time_point t0) {
     ctx->src.active = false;
     if (!base) return fail(ctx, RT_E_INVALID, "base scene is null");
     if (mesh_count < 0 || (mesh_count && !meshes)) return fail(ctx, RT_E_INVALID, "bad mesh source array");
@@ -1148,9 +1721,8 @@ int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_so
     return RT_OK;
 }
 
-int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count) {
-    if (!ctx) return RT_E_INVALID;
-    const auto t0 = std::chrono::steady_clock::now();
+int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count,
+                              std::chrono::steady_clock::time_point t0) {
     if (!ctx->has_scene || !ctx->src.active)
         return fail(ctx, RT_E_STATE, "rt_update_mesh_transforms needs a scene from rt_set_scene_source");
     if (mesh_count != ctx->src.mesh_count || (mesh_count && !local_to_world))
@@ -1199,6 +1771,26 @@ int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t 
     return RT_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count) {
+    if (!ctx) return RT_E_INVALID;
+    Range range("rt_set_scene_source");
+    DeviceGuard guard;
+    const auto t0 = std::chrono::steady_clock::now();
+    return for_members(ctx, [&](rt_ctx *m) { return set_scene_source_one(m, base, meshes, mesh_count, t0); });
+}
+
+int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count) {
+    if (!ctx) return RT_E_INVALID;
+    Range range("rt_update_mesh_transforms");
+    DeviceGuard guard;
+    const auto t0 = std::chrono::steady_clock::now();
+    return for_members(ctx, [&](rt_ctx *m) { return update_mesh_transforms_one(m, local_to_world, mesh_count, t0); });
+}
+
 int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info) {
     if (!ctx || !info) return RT_E_INVALID;
     if (!ctx->has_scene) return RT_E_STATE;
@@ -1208,19 +1800,29 @@ int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info) {
 
 int rt_finish(rt_ctx *ctx, rt_stats *stats) {
     if (!ctx) return RT_E_INVALID;
-    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    const int st = settle_async(ctx);
-    if (st) return st;
-    if (stats) {
-        const double wall = ctx->async_t0_set ? std::chrono::duration<double, std::milli>(
-                                                    std::chrono::steady_clock::now() - ctx->async_t0)
-                                                    .count()
-                                              : 0.0;
-        fill_stats(stats, ctx->async_acc, ctx->async_ms, wall);
+    DeviceGuard guard;
+    // a multi-device context: every member's frames; device time = the slowest member's
+    unsigned long long sum[rtd::kCounterWords] = {0};
+    double kms = 0.0;
+    const bool t0_set = ctx->async_t0_set;
+    const auto t0 = ctx->async_t0;
+    for (int i = 0; i < nmembers(ctx); ++i) {
+        rt_ctx *m = member(ctx, i);
+        unsigned long long c[rtd::kCounterWords];
+        double ms = 0.0;
+        const int st = take_async(m, c, ms);
+        if (st) {
+            if (i) ctx->err = m->err;
+            return st;
+        }
+        for (int w = 0; w < rtd::kCounterWords; ++w) sum[w] += c[w];
+        kms = std::max(kms, ms);
     }
-    for (int w = 0; w < rtd::kCounterWords; ++w) ctx->async_acc[w] = 0;
-    ctx->async_ms = 0.0;
-    ctx->async_t0_set = false;
+    if (stats) {
+        const double wall =
+            t0_set ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() : 0.0;
+        fill_stats(stats, sum, kms, wall);
+    }
     return RT_OK;
 }
 
@@ -1233,19 +1835,28 @@ int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
               void *out_rgba, rt_stats *stats) {
     if (!ctx) return RT_E_INVALID;
     auto t0 = std::chrono::steady_clock::now();
+    Range range("rt_render");
+    DeviceGuard guard;
+    if (params && (params->flags & RT_FLAG_ASYNC))
+        return fail(ctx, RT_E_INVALID, "RT_FLAG_ASYNC needs a device output (rt_render_device)");
+    const bool group = !ctx->peers.empty() || ctx->gather == RT_GATHER_RCCL;
+    if (group && params && params->band_count <= 1) {
+        if (!camera || !plane) return fail(ctx, RT_E_INVALID, "null camera/plane/params");
+        if (plane->resolution_x < 0 || plane->resolution_y < 0)
+            return fail(ctx, RT_E_INVALID, "negative resolution (%d, %d)", plane->resolution_x, plane->resolution_y);
+        const size_t bytes = (size_t)plane->resolution_x * plane->resolution_y * rt_pixel_bytes(params->flags);
+        if (bytes && !out_rgba) return fail(ctx, RT_E_INVALID, "out_rgba is null");
+        HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+        HIP_OR_FAIL(ctx, ensure_out(ctx, bytes));
+        return group_frame(ctx, camera, plane, params, ctx->d_out, out_rgba, bytes, stats, t0);
+    }
     rtd::FrameDev F;
     size_t bytes = 0;
     int st = prepare_frame(ctx, camera, plane, params, F, bytes);
     if (st) return st;
     if (bytes && !out_rgba) return fail(ctx, RT_E_INVALID, "out_rgba is null");
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    if (bytes > ctx->d_out_cap) {
-        if (ctx->d_out) HIP_OR_FAIL(ctx, hipFree(ctx->d_out));
-        ctx->d_out = nullptr;
-        ctx->d_out_cap = 0;
-        HIP_OR_FAIL(ctx, hipMalloc(&ctx->d_out, bytes));
-        ctx->d_out_cap = bytes;
-    }
+    HIP_OR_FAIL(ctx, ensure_out(ctx, bytes));
     return run_frame(ctx, F, params, ctx->d_out, stats, t0, out_rgba, bytes);
 }
 
@@ -1253,6 +1864,18 @@ int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane 
                      const rt_render_params *params, void *d_out_rgba, size_t out_bytes, rt_stats *stats) {
     if (!ctx) return RT_E_INVALID;
     auto t0 = std::chrono::steady_clock::now();
+    DeviceGuard guard;
+    const bool group = !ctx->peers.empty() || ctx->gather == RT_GATHER_RCCL;
+    if (group && params && params->band_count <= 1) {
+        if (!camera || !plane) return fail(ctx, RT_E_INVALID, "null camera/plane/params");
+        if (plane->resolution_x < 0 || plane->resolution_y < 0)
+            return fail(ctx, RT_E_INVALID, "negative resolution (%d, %d)", plane->resolution_x, plane->resolution_y);
+        const size_t bytes = (size_t)plane->resolution_x * plane->resolution_y * rt_pixel_bytes(params->flags);
+        if (bytes && !d_out_rgba) return fail(ctx, RT_E_INVALID, "d_out_rgba is null");
+        if (out_bytes < bytes)
+            return fail(ctx, RT_E_INVALID, "output buffer %zu bytes < %zu required", out_bytes, bytes);
+        return group_frame(ctx, camera, plane, params, d_out_rgba, nullptr, 0, stats, t0);
+    }
     rtd::FrameDev F;
     size_t bytes = 0;
     int st = prepare_frame(ctx, camera, plane, params, F, bytes);
@@ -1291,8 +1914,14 @@ int rt_assemble_bands_ex(rt_ctx *ctx, const void *d_gathered, int32_t resolution
 
 int rt_synchronize(rt_ctx *ctx) {
     if (!ctx) return RT_E_INVALID;
+    DeviceGuard guard;
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    for (const GroupSlot &g : ctx->gslots)
+        for (size_t i = 1; g.used && i < g.member_stream.size(); ++i) {
+            HIP_OR_FAIL(ctx, hipSetDevice(member(ctx, (int)i)->device));
+            HIP_OR_FAIL(ctx, hipStreamSynchronize(g.member_stream[i]));
+        }
     return RT_OK;
 }
 
@@ -1334,12 +1963,22 @@ int rt_intersect_rays(rt_ctx *ctx, const rt_ray *rays, int32_t n, rt_hit *out_hi
             h.type = 3;
             h.mesh_index = m;
             h.index = rk - f[m];
-        } else if (rk < ctx->mesh_tri_ranks + ctx->sphere_count) {
-            h.type = 1;
-            h.index = rk - ctx->mesh_tri_ranks;
         } else {
-            h.type = 2;
-            h.index = rk - ctx->mesh_tri_ranks - ctx->sphere_count;
+            if (rk < ctx->mesh_tri_ranks + ctx->sphere_count) {
+                h.type = 1;
+                h.index = rk - ctx->mesh_tri_ranks;
+            } else {
+                h.type = 2;
+                h.index = rk - ctx->mesh_tri_ranks - ctx->sphere_count;
+            }
+            // a sphere / loose triangle won after a mesh triangle had been the
+            // running closest hit: the reference keeps that mesh's index
+            // (Scene.cs:76-79 set it, :94-97 and :109-112 never reset it)
+            const int mr = hits[i].z;
+            if (mr >= 0 && mr < ctx->mesh_tri_ranks) {
+                const auto &f = ctx->mesh_rank_first;
+                h.mesh_index = (int)(std::upper_bound(f.begin(), f.end() - 1, mr) - f.begin()) - 1;
+            }
         }
     }
     return RT_OK;

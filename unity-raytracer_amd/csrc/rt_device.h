@@ -153,6 +153,17 @@ struct SceneDev {
     float spec_threshold;  // d < spec_threshold  <=>  degrees(acos(d)) > 90f
 };
 
+// Longest-first dispatch key of one tile (render_kernel): its shader-clock
+// cost on a log scale (4 mantissa bits, < 512, one cheap radix-sort pass set).
+// A tile split into 64 >> pshift parts is measured on its first part and
+// charged that part's cost times the number of parts.
+__host__ __device__ __forceinline__ unsigned tile_cost_key(unsigned long long c64, int part, int pshift) {
+    if (part == 0) c64 <<= 6 - pshift;  // parts = 64 >> pshift
+    const unsigned c = (unsigned)(c64 < 0xffffffffull ? c64 : 0xffffffffull);
+    const unsigned e = c ? 31u - (unsigned)__builtin_clz(c) : 0u;  // floor(log2 c)
+    return e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
+}
+
 // Per-frame constants of CastPixelRays (RayTracingSetup.cs:277-284).
 struct FrameDev {
     float cam_pos[3];
@@ -166,6 +177,7 @@ struct FrameDev {
     int max_bounces;
     int band_index, band_count, band_rows;
     int local_rows;          // rows of the compact output buffer
+    int row0;                // band_count == 1: first image row of this launch (a row slab of rt_render)
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
     void *out;               // local_rows x res_x pixels in out_format

@@ -200,7 +200,7 @@ __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int
     const int tx = tile % F.tiles_x, ty = tile / F.tiles_x;
     px = tx * F.tile_w + pix % F.tile_w;
     ly = ty * F.tile_h + pix / F.tile_w;
-    gy = ly;
+    gy = ly + F.row0;
     if (F.band_count > 1) {
         const int blk = ly / F.band_rows;
         gy = (blk * F.band_count + F.band_index) * F.band_rows + (ly - blk * F.band_rows);

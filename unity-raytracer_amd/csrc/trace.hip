@@ -185,6 +185,11 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
         f3 o, d;
         rts::primary_ray(F, px, gy, s, o, d);
         cnt.primary += 1;
+        if (COUNT) {  // trivially cheap camera samples: they miss Scene.AABB (Scene.cs:54)
+            rtt::RayCtx rg;
+            rtt::setup_ray(rg, o, d);
+            cnt.scene_miss += !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
+        }
         color = shade_path<COUNT>(S, F, o, d, st, wstack, cnt, sg);
     }
     const f3 sum = rts::sample_sum(color, lane, F.spp);
@@ -269,13 +274,7 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     }
 #endif
     if (F.tile_cost && lane == 0 && part <= 0) {
-        // log-scale cost key (4 mantissa bits, < 512): one cheap sort pass
-        // set; a split tile is charged its first part times the parts
-        unsigned long long c64 = __builtin_amdgcn_s_memtime() - t0;
-        if (part == 0) c64 <<= 8 - pshift;
-        const unsigned c = (unsigned)min(c64, 0xffffffffull);
-        const unsigned e = c ? 31u - __clz(c) : 0u;
-        F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
+        F.tile_cost[tile] = tile_cost_key(__builtin_amdgcn_s_memtime() - t0, part, pshift);
     }
     rtt::flush_counts<COUNT>(cnt, F.counters);
 }
@@ -396,7 +395,16 @@ __global__ __launch_bounds__(kBlockThreads) void intersect_kernel(SceneDev S, co
     int br;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     rtt::traverse<false, false>(S, r, 0.0f, 0.0f, bt, br, st, cnt);
-    out[i] = make_int4(br, __float_as_int(bt), 0, 0);
+    // ObjectId.MeshIndex: the reference sets it only when a mesh triangle
+    // becomes the running closest hit and never resets it when a sphere or a
+    // loose triangle wins later (Scene.cs:76-79 vs :94-97,:109-112), so for
+    // such a winner it is the mesh of the closest mesh-triangle hit, if any.
+    int mesh_rank = br >= 0 && br < S.mesh_tri_total ? br : -1;
+    if (br >= S.mesh_tri_total && S.mesh_tri_total > 0) {
+        float mt;
+        rtt::traverse<false, false, true>(S, r, 0.0f, 0.0f, mt, mesh_rank, st, cnt);
+    }
+    out[i] = make_int4(br, __float_as_int(bt), mesh_rank, 0);
 }
 
 struct Px12 {  // float RGB pixel (RT_FLAG_OUT_RGB32F)

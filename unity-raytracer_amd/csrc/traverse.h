@@ -22,6 +22,7 @@ using rtm::mk;
 
 struct Counts {
     unsigned primary, shadow, reflection, box, tri, sph, shading;
+    unsigned scene_miss;  // camera samples rejected by the scene AABB gate (Scene.cs:54), COUNT launches
 };
 
 __device__ __forceinline__ float nudge(float v) { return fabsf(v) > 1e-20f ? v : copysignf(1e-20f, v); }
@@ -103,17 +104,9 @@ struct Stack {
     int *ovf;
 };
 
-// RT_OVF_VOLATILE: volatile overflow accesses compile to system-coherent
-// (sc0 sc1) flat stores/loads that bypass the caches — every overflowing push
-// became an HBM write.  Plain private accesses stay in scratch (L1/L2).
-#ifndef RT_OVF_VOLATILE
-#define RT_OVF_VOLATILE 1
-#endif
-#if RT_OVF_VOLATILE
+// Overflow accesses are volatile so the compiler never folds the LDS and
+// private loads into one generic (flat) load.
 typedef volatile int ovf_int;
-#else
-typedef int ovf_int;
-#endif
 
 __device__ __forceinline__ void push(Trav &t, const Stack &st, int v) {
     if (t.sp < rtd::kStackSize)
@@ -229,25 +222,18 @@ __device__ __forceinline__ bool tri_rec(const RayCtx &r, Trav &t, float d2, cons
     return false;
 }
 
-// Triangle leaf with the records fetched up front (indices clamped to the
+// Triangle leaf with the records fetched in pairs (indices clamped to the
 // leaf, so the loads are unconditional and issue back to back): one memory
-// latency per leaf (RT_LEAF_BATCH 1: all four) or per pair of triangles
-// (RT_LEAF_BATCH 2) instead of one per triangle; the gate comes from the
-// first record.
-#ifndef RT_LEAF_BATCH
-#define RT_LEAF_BATCH 2
-#endif
-template <bool ANY, bool COUNT>
+// latency per pair of triangles instead of one per triangle; the gate comes
+// from the first record.
+template <bool ANY, bool COUNT, bool MESH_ONLY = false>
 __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
                                                   int first, int count, Counts &cnt) {
     const rtd::TriRec *b = S.tris + first;
     const rtd::TriRec t0 = b[0];
     const rtd::TriRec t1 = b[count > 1 ? 1 : 0];
-#if RT_LEAF_BATCH == 1
-    const rtd::TriRec t2 = b[count > 2 ? 2 : 0];
-    const rtd::TriRec t3 = b[count > 3 ? 3 : 0];
-#endif
     const int gate = __float_as_int(t0.p2.z);
+    if (MESH_ONLY && gate < 0) return false;  // a loose-triangle leaf (leaves are homogeneous in mesh)
     if (gate >= 0) {
         if (gate != t.gate_cached) {
             t.gate_cached = gate;
@@ -259,16 +245,12 @@ __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const 
     }
     if (tri_rec<ANY, COUNT>(r, t, d2, t0, cnt)) return true;
     if (count > 1 && tri_rec<ANY, COUNT>(r, t, d2, t1, cnt)) return true;
-#if RT_LEAF_BATCH != 1  // pairs: the second pair is fetched together after the first
-    if (count > 2) {
+    if (count > 2) {  // the second pair, fetched together after the first
         const rtd::TriRec t2 = b[2];
         const rtd::TriRec t3 = b[count > 3 ? 3 : 2];
-#endif
-        if (count > 2 && tri_rec<ANY, COUNT>(r, t, d2, t2, cnt)) return true;
+        if (tri_rec<ANY, COUNT>(r, t, d2, t2, cnt)) return true;
         if (count > 3 && tri_rec<ANY, COUNT>(r, t, d2, t3, cnt)) return true;
-#if RT_LEAF_BATCH != 1
     }
-#endif
     return false;
 }
 
@@ -316,7 +298,10 @@ __device__ __forceinline__ float child_key_nf(float nx, float fx, float ny, floa
 // Returns true when the query is complete.  ANY: t.best_rank = 1 iff a hit
 // with t*t < d2 exists — equivalent to the reference's closest-hit-then-
 // compare (RayTracingSetup.cs:333-345) since t >= 0 makes t -> t*t monotone.
-template <bool ANY, bool COUNT>
+// MESH_ONLY: closest hit among mesh triangles only (sphere and loose-triangle
+// leaves skipped) — the running winner of the reference's mesh loop, whose
+// MeshIndex survives a later sphere/loose-triangle win (Scene.cs:64-85,94-97).
+template <bool ANY, bool COUNT, bool MESH_ONLY = false>
 __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
                                           const Stack &st, Counts &cnt) {
     if (t.node >= 0 && S.bvh4) {
@@ -377,9 +362,9 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         const int first = v & ((1 << rtd::kLeafFirstBits) - 1);
         const int count = ((v >> rtd::kLeafFirstBits) & 3) + 1;
         const int kind = (v >> (rtd::kLeafFirstBits + 2)) & 1;
-        if (RT_LEAF_BATCH && kind == rtd::kLeafTri) {
-            if (leaf_tris_batched<ANY, COUNT>(S, r, t, d2, first, count, cnt)) return true;
-        } else {
+        if (kind == rtd::kLeafTri) {
+            if (leaf_tris_batched<ANY, COUNT, MESH_ONLY>(S, r, t, d2, first, count, cnt)) return true;
+        } else if (!MESH_ONLY) {
             const int gate = kind == rtd::kLeafTri ? __float_as_int(S.tris[first].p2.z) : S.sphs[first].misc.y;
             if (leaf<ANY, COUNT>(S, r, t, d2, first, count, kind, gate, cnt)) return true;
         }
@@ -390,7 +375,7 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
 #undef RT_CSWAP
 
 // Whole query in one call (megakernel / batch-intersect path).
-template <bool ANY, bool COUNT>
+template <bool ANY, bool COUNT, bool MESH_ONLY = false>
 __device__ __forceinline__ bool traverse(const rtd::SceneDev &S, const RayCtx &r, float tlimit, float d2,
                                          float &best_t, int &best_rank, const Stack &st, Counts &cnt) {
     Trav t;
@@ -399,7 +384,7 @@ __device__ __forceinline__ bool traverse(const rtd::SceneDev &S, const RayCtx &r
         best_rank = -1;
         return false;
     }
-    while (!trav_step<ANY, COUNT>(S, r, t, d2, st, cnt)) {
+    while (!trav_step<ANY, COUNT, MESH_ONLY>(S, r, t, d2, st, cnt)) {
     }
     best_t = t.best_t;
     best_rank = t.best_rank;
@@ -418,12 +403,13 @@ template <bool COUNT>
 __device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long *counters) {
     unsigned long long *ctr = counters + (size_t)(blockIdx.x % rtd::kCounterSlots) * rtd::kCounterWords;
     const unsigned p = wave_sum(c.primary), s = wave_sum(c.shadow), r = wave_sum(c.reflection);
-    unsigned b = 0, t = 0, q = 0, h = 0;
+    unsigned b = 0, t = 0, q = 0, h = 0, g = 0;
     if (COUNT) {
         b = wave_sum(c.box);
         t = wave_sum(c.tri);
         q = wave_sum(c.sph);
         h = wave_sum(c.shading);
+        g = wave_sum(c.scene_miss);
     }
     if ((threadIdx.x & 63) == 0) {
         if (p) atomicAdd(ctr + 0, (unsigned long long)p);
@@ -434,6 +420,7 @@ __device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long
             if (t) atomicAdd(ctr + 4, (unsigned long long)t);
             if (q) atomicAdd(ctr + 5, (unsigned long long)q);
             if (h) atomicAdd(ctr + 6, (unsigned long long)h);
+            if (g) atomicAdd(ctr + 7, (unsigned long long)g);
         }
     }
 }

@@ -73,12 +73,20 @@ def frame_params(fr: Frame, **kw) -> abi.rt_render_params:
 
 
 class Context:
-    """Owns one rt_ctx (one GPU).  Thin, error-checked wrapper of the C-ABI."""
+    """Owns one rt_ctx.  Thin, error-checked wrapper of the C-ABI.
 
-    def __init__(self, num_gpus: int = 1, lib_path: Optional[str] = None):
+    num_gpus > 1 (or an explicit ``devices`` list, repeats = logical shards on
+    one GPU) gives one context that renders every frame on all of them: row
+    bands per device, gathered to devices[0] (RCCL or peer copies)."""
+
+    def __init__(self, num_gpus: int = 1, lib_path: Optional[str] = None, devices=None, gather: int = 0):
         self.lib = abi.load_library(lib_path)
         h = C.c_void_p()
-        st = self.lib.rt_create(C.byref(h), int(num_gpus))
+        if devices is not None:
+            arr = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            st = self.lib.rt_create_devices(C.byref(h), C.cast(arr, C.c_void_p), len(devices), int(gather))
+        else:
+            st = self.lib.rt_create(C.byref(h), int(num_gpus))
         if st != abi.RT_OK:
             raise abi.RtError(st, self.lib.rt_last_error(None).decode())
         self.h = h
@@ -98,6 +106,12 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def device_info(self) -> dict:
+        info = abi.rt_device_info()
+        self._check(self.lib.rt_get_device_info(self.h, C.byref(info)))
+        return {"num_devices": info.num_devices, "gather": info.gather,
+                "devices": list(info.devices)[:min(16, info.num_devices)]}
 
     def set_stream(self, stream_handle: int):
         self._check(self.lib.rt_set_stream(self.h, C.c_void_p(stream_handle)))
