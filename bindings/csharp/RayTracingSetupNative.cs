@@ -28,6 +28,7 @@ namespace RayTracer.Native
         public int MaxReflectionBounces = 1;
         public int SamplesPerPixel = 1;          // n*n; 1 == the reference
         public bool OutputRgba8;
+        public int NumGpus = 1;                  // > 1: row bands on that many GPUs, gathered to GPU 0 in the library
 
         public Color[] PixelColors = Array.Empty<Color>();
         public Color32[] PixelColors32 = Array.Empty<Color32>();
@@ -41,7 +42,7 @@ namespace RayTracer.Native
 
         void Start()
         {
-            if (Rt.rt_create(out _rt, 1) != Rt.OK)
+            if (Rt.rt_create(out _rt, NumGpus) != Rt.OK)
                 Debug.LogError(Rt.LastError(IntPtr.Zero));
         }
 
