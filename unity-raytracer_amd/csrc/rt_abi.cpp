@@ -327,9 +327,6 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     if (n < 0 || n > 8)
         return fail(ctx, RT_E_INVALID, "samples_per_pixel must be n*n with 1 <= n <= 8, got %d",
                     prm->samples_per_pixel);
-    if (prm->max_reflection_bounces > rtd::kMaxBounces)
-        return fail(ctx, RT_E_INVALID, "max_reflection_bounces %d > %d unsupported", prm->max_reflection_bounces,
-                    rtd::kMaxBounces);
     const int band_count = prm->band_count <= 0 ? 1 : prm->band_count;
     const int band_rows = prm->band_rows <= 0 ? 8 : prm->band_rows;
     if (prm->band_index < 0 || prm->band_index >= band_count)
@@ -624,7 +621,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // the most expensive tiles of the last measurement are split into
     // quarter-waves (a frame's time is bounded below by its slowest wave);
     // render_kernel only: 16 lanes must hold whole pixels
-    const bool levels = ctx->S.bvh4 && F.spp >= 16;
+    const bool levels = (ctx->S.bvh4 && F.spp >= 16) || F.max_bounces > rtd::kMaxBounces;  // (or deep: no splits)
     if (F.tile_order && !count && !levels && kSplitDiv > 0 && 16 % F.spp == 0 && F.num_tiles <= kSplitMaxTiles) {
         F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
         // sixteenth-waves (4 lanes) must hold whole pixels too
@@ -655,8 +652,11 @@ struct Path {
 Path frame_path(const rt_ctx *ctx, const rt_render_params *prm) {
     Path p;
     p.count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
-    p.packet = (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
-    p.wavefront = !p.packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
+    // MaxReflectionBounces beyond the fold stack: only the megakernel's
+    // deep-chain instance folds unbounded chains
+    const bool deep = prm->max_reflection_bounces > rtd::kMaxBounces;
+    p.packet = !deep && (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
+    p.wavefront = !deep && !p.packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
     p.mega = !p.packet && !p.wavefront;  // default
     return p;
 }

@@ -62,14 +62,124 @@ struct SegClock {
     unsigned long long setup, prim, shadow, visits;
 };
 
+// Ambient + every point light of one hit (RayTracingSetup.cs:320-356), shadow
+// rays traced per lane.
+template <bool COUNT>
+__device__ __forceinline__ f3 shade_hit(const SceneDev &S, const rts::Surface &sf, const rtt::Stack &st,
+                                        Counts &cnt) {
+    f3 col = rts::ambient(S, S.mats[sf.mat]);
+    for (int l = 0; l < S.num_lights; ++l) {  // :327-356
+        const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
+        cnt.shadow++;
+        rtt::RayCtx rs;
+        rtt::setup_ray(rs, sr.o, sr.dir);
+        float dt;
+        int dr;
+        if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) continue;
+        col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+    }
+    return col;
+}
+
+// One level of a mirror chain without shading: the closest hit of (o, d) and,
+// if it is a mirror below MaxReflectionBounces, the reflected ray (o, d
+// updated).  0: miss, 1: mirror bounce, 2: the chain ends at this hit (sf).
+template <bool COUNT>
+__device__ __forceinline__ int walk_level(const SceneDev &S, const FrameDev &F, f3 &o, f3 &d, int level,
+                                          const rtt::Stack &st, Counts &cnt, rts::Surface &sf) {
+    rtt::RayCtx r;
+    rtt::setup_ray(r, o, d);
+    float bt;
+    int br;
+    if (!rtt::traverse<false, COUNT>(S, r, 0.0f, 0.0f, bt, br, st, cnt)) return 0;
+    if (COUNT) cnt.shading++;
+    sf = rts::surface(S, o, d, bt, br);
+    if (S.mats[sf.mat].ka_mirror.w != 0.0f && level < F.max_bounces) {
+        rts::reflect(sf, o, d);
+        return 1;
+    }
+    return 2;
+}
+
+// A mirror chain deeper than the fold stack (MaxReflectionBounces > kMaxBounces,
+// RayTracingSetup.cs:23,358: an unbounded int in the reference).  The chain
+// from level l0 (ray o0/d0) has already been shaded and counted up to level
+// lc = l0 + kMaxBounces, where (oc, dc) is the ray.  Same rounding as the
+// recursion with O(kMaxBounces) storage: (1) walk from lc to the end of the
+// chain (closest hits only) and shade its last hit; (2) from the deepest
+// segment of kMaxBounces levels up, re-walk from (o0, d0) to the segment's
+// first level, shade the segment's levels into the fold stack and fold them
+// onto the running value.  Re-walks are deterministic, so they rebuild the
+// same rays bit for bit; every reference ray is counted once (levels below lc
+// were counted by the caller).
+template <bool COUNT>
+__device__ __noinline__ f3 deep_chain(const SceneDev &S, const FrameDev &F, f3 o0, f3 d0, int l0, f3 oc, f3 dc,
+                                      const rtt::Stack &st, Counts &cnt) {
+    const int lc = l0 + kMaxBounces;
+    Counts none = {0, 0, 0, 0, 0, 0, 0, 0};
+    rts::Surface sf;
+    f3 term;
+    int end = lc;  // level of the chain's last ray
+    {
+        f3 o = oc, d = dc;
+        while (true) {
+            const int k = walk_level<COUNT>(S, F, o, d, end, st, cnt, sf);
+            if (k == 0) {
+                term = rtt::ld3(F.bg255);  // :310-311
+                break;
+            }
+            if (k == 2) {
+                term = shade_hit<COUNT>(S, sf, st, cnt);
+                break;
+            }
+            cnt.reflection++;
+            ++end;
+        }
+    }
+    // levels l0 .. end-1 are mirror bounces; fold them in segments, deepest first
+    float fold_c[kMaxBounces][3];
+    float fold_k[kMaxBounces][3];
+    for (int seg = l0 + ((end - 1 - l0) / kMaxBounces) * kMaxBounces; seg >= l0; seg -= kMaxBounces) {
+        f3 o = o0, d = d0;
+        int level = l0;
+        if (seg >= lc) {
+            o = oc;
+            d = dc;
+            level = lc;
+        }
+        for (; level < seg; ++level) (void)walk_level<COUNT>(S, F, o, d, level, st, none, sf);
+        const int seg_end = min(seg + kMaxBounces, end);
+        for (; level < seg_end; ++level) {
+            rtt::RayCtx r;
+            rtt::setup_ray(r, o, d);
+            float bt;
+            int br;
+            (void)rtt::traverse<false, COUNT>(S, r, 0.0f, 0.0f, bt, br, st, none);  // a mirror hit
+            const rts::Surface sfl = rts::surface(S, o, d, bt, br);
+            const f3 col = level >= lc ? shade_hit<COUNT>(S, sfl, st, cnt) : shade_hit<COUNT>(S, sfl, st, none);
+            const DevMaterial m = S.mats[sfl.mat];
+            const int i = level - seg;
+            fold_c[i][0] = col.x; fold_c[i][1] = col.y; fold_c[i][2] = col.z;
+            fold_k[i][0] = m.km.x; fold_k[i][1] = m.km.y; fold_k[i][2] = m.km.z;
+            rts::reflect(sfl, o, d);
+        }
+        for (int i = seg_end - seg - 1; i >= 0; --i)
+            term = mk(fold_c[i][0], fold_c[i][1], fold_c[i][2]) + mk(fold_k[i][0], fold_k[i][1], fold_k[i][2]) * term;
+    }
+    return term;
+}
+
 // Shade levels depth0.. of one sample with per-lane traversal: the mirror
 // recursion unrolled into a loop, its results folded back to front so
-// c + km*(c' + km'*(...)) rounds exactly like the reference.
-template <bool COUNT>
+// c + km*(c' + km'*(...)) rounds exactly like the reference.  DEEP (frames with
+// MaxReflectionBounces > kMaxBounces only): a chain that outgrows the fold
+// stack continues in deep_chain.
+template <bool COUNT, bool DEEP>
 __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F, f3 o, f3 d, int depth0,
                                            const rtt::Stack &st, Counts &cnt) {
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
+    const f3 o0 = o, d0 = d;
     int depth = depth0;
     f3 term;
     while (true) {
@@ -83,17 +193,11 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
         }
         if (COUNT) cnt.shading++;
         const rts::Surface sf = rts::surface(S, o, d, bt, br);
-        f3 col = rts::ambient(S, S.mats[sf.mat]);
-        for (int l = 0; l < S.num_lights; ++l) {  // :327-356
-            const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
-            cnt.shadow++;
-            rtt::RayCtx rs;
-            rtt::setup_ray(rs, sr.o, sr.dir);
-            float dt;
-            int dr;
-            if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) continue;
-            col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+        if (DEEP && depth - depth0 == kMaxBounces && S.mats[sf.mat].ka_mirror.w != 0.0f && depth < F.max_bounces) {
+            if (COUNT) cnt.shading--;  // deep_chain counts this hit again
+            return deep_chain<COUNT>(S, F, o0, d0, depth0, o, d, st, cnt);
         }
+        const f3 col = shade_hit<COUNT>(S, sf, st, cnt);
         const DevMaterial m = S.mats[sf.mat];
         if (m.ka_mirror.w != 0.0f && depth < F.max_bounces) {  // :358-363
             fold_c[depth - depth0][0] = col.x; fold_c[depth - depth0][1] = col.y; fold_c[depth - depth0][2] = col.z;
@@ -117,11 +221,11 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 // shadow rays to each light: packet.h, scalar node fetches); the mirror
 // chain below it (a few percent of samples) runs per lane (shade_levels).
 // The counting launch keeps the per-ray traversal's canonical counts.
-template <bool COUNT>
+template <bool COUNT, bool DEEP>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
                                          int *wstack, Counts &cnt, SegClock &sg) {
     (void)sg;
-    if (COUNT || !S.bvh4) return shade_levels<COUNT>(S, F, o, d, 0, st, cnt);
+    if (COUNT || !S.bvh4) return shade_levels<COUNT, DEEP>(S, F, o, d, 0, st, cnt);
     RT_SEG(const unsigned long long tq0 = __builtin_amdgcn_s_memtime();)
     rtt::RayCtx r;
     rtt::setup_ray(r, o, d);
@@ -150,7 +254,7 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         cnt.reflection++;
         f3 ro, rd;
         rts::reflect(sf, ro, rd);
-        const f3 below = shade_levels<COUNT>(S, F, ro, rd, 1, st, cnt);
+        const f3 below = shade_levels<COUNT, DEEP>(S, F, ro, rd, 1, st, cnt);
         return col + mk(m.km.x, m.km.y, m.km.z) * below;
     }
     return col;
@@ -174,7 +278,7 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
 // one of the four (pshift 4: 16 lanes) or sixteen (pshift 2: 4 lanes) waves
 // an expensive tile is split into.
-template <bool COUNT>
+template <bool COUNT, bool DEEP>
 __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
                                             SegClock &sg) {
@@ -190,7 +294,7 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
             rtt::setup_ray(rg, o, d);
             cnt.scene_miss += !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
         }
-        color = shade_path<COUNT>(S, F, o, d, st, wstack, cnt, sg);
+        color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg);
     }
     const f3 sum = rts::sample_sum(color, lane, F.spp);
     // the slot -> pixel mapping is recomputed from the (scalar) tile index
@@ -206,8 +310,9 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
 }
 
 // SPLIT: the variant launched when a frame splits tiles (a separate instance, so
-// the common kernel's code and register allocation stay as they are).
-template <bool COUNT, bool SPLIT = false>
+// the common kernel's code and register allocation stay as they are); DEEP:
+// the one for MaxReflectionBounces > kMaxBounces (deep_chain).
+template <bool COUNT, bool SPLIT = false, bool DEEP = false>
 __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
     constexpr bool kPackets = RT_MK_PACKET_SHADOW || RT_MK_PACKET_PRIMARY;
@@ -243,7 +348,7 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    render_tile<COUNT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    render_tile<COUNT, DEEP>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
 #ifdef RT_SEG_PROFILE
     if (!COUNT) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -441,7 +546,12 @@ namespace rtk {
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
     const int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
-    if (count_tests)
+    if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
+        if (count_tests)
+            hipLaunchKernelGGL((render_kernel<true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+        else
+            hipLaunchKernelGGL((render_kernel<false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+    } else if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (F.split_tiles > 0 || F.split16_tiles > 0)
         hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);

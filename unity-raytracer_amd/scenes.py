@@ -267,6 +267,37 @@ def cornell_c2() -> Frame:
                  background=(0.0, 0.0, 0.0, 1.0), max_bounces=8, spp=4)
 
 
+def mirror_corridor(depth=40, res=(24, 12), spp=1, loose=True) -> Frame:
+    """Two facing mirror walls (x = -1, x = +1; km 0.9, 0.8, 0.7) along a
+    400-unit corridor with a white floor, a mirror sphere, a point light and an
+    ambient light; the camera looks down the corridor through a wide image
+    plane, so rays bounce between the walls tens of times — mirror chains
+    deeper than the library's 32-entry fold stack (MaxReflectionBounces is an
+    unbounded int in the reference, RayTracingSetup.cs:23,358).  loose=False:
+    the walls as one mesh (SceneMesh) instead of loose triangles."""
+    wall = MaterialData(DiffuseReflectance=(0.2, 0.2, 0.2), AmbientReflectance=(0.05, 0.05, 0.05),
+                        MirrorReflectance=(0.9, 0.8, 0.7), SpecularReflectance=(0.3, 0.3, 0.3),
+                        PhongExponent=16.0, IsMirror=True)
+    sc = Scene()
+    tris, mats = [], []
+    L = 200.0
+    _oriented_quad((-1, -1, -L), (-1, -1, L), (-1, 1, L), (-1, 1, -L), (0, 0, 0), wall, tris, mats, loose)
+    _oriented_quad((1, -1, -L), (1, -1, L), (1, 1, L), (1, 1, -L), (0, 0, 0), wall, tris, mats, loose)
+    _oriented_quad((-1, -1, -L), (1, -1, -L), (1, -1, L), (-1, -1, L), (0, 0, 0), WHITE, tris, mats, True)
+    t = np.concatenate(tris)
+    if loose:
+        sc.add_triangles(t, mats)
+    else:
+        sc.add_mesh(_mesh_from_tris(t[:4], t[:4].reshape(-1, 3), wall))
+        sc.add_triangles(t[4:], mats[4:])
+    sc.add_sphere_r2((0.3, -0.5, 12.0), 0.25, MIRROR)
+    sc.add_point_light((0.0, 0.9, 4.0), 300.0)
+    sc.AmbientLight = np.array(AMBIENT, f32)
+    cam = CameraData(Position=(0.1, 0.05, -3.4))
+    return Frame(f"corridor{depth}", sc, cam, ImagePlane(res[0], res[1], 1.0, 2.5, 0.08),
+                 background=(0.1, 0.2, 0.3, 1.0), max_bounces=depth, spp=spp)
+
+
 def torus_knot(p=2, q=3, segments=384, sides=90, scale=0.22, tube=0.085, center=(0.0, -0.15, 0.15)):
     """(p,q) torus-knot tube: segments x sides quads = 2*segments*sides tris."""
     phi = np.arange(segments, dtype=np.float64) * (2 * np.pi / segments)
