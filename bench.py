@@ -561,7 +561,7 @@ def main():
     if rank == 0:
         avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's own trace kernel, HIP events
         pmc, pmc_state = load_pmc(args.config, lib_path)
-        kname = {"megakernel": "render_kernel<false, false>", "packet": "render_packet_kernel<false, 1>"}.get(
+        kname = {"megakernel": "render_kernel<false, false, false>", "packet": "render_packet_kernel<false, 1>"}.get(
             args.mode, "wavefront passes (sum)")
         rays_per_frame = rays // args.steps
         line = {
