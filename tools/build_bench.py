@@ -36,8 +36,9 @@ def main():
                 ctx.set_scene(fr.scene, build)
                 infos.append(ctx.scene_info())
             times = []
+            out = torch.empty((fr.plane.ResolutionY, fr.plane.ResolutionX, 4), dtype=torch.float32, device="cuda")
             for _ in range(a.frames):
-                _, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+                st = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr), out.data_ptr(), out.numel() * 4)
                 times.append(st.kernel_ms)
             rec = {"config": name, "variant": a.variant or "default", "build": label, "primitives": infos[-1]["primitives"],
                    "nodes": infos[-1]["nodes"],
@@ -56,7 +57,8 @@ def main():
         for k in range(1, a.reps + 1):
             ctx.update_mesh_transforms(ms[k])
             infos.append(ctx.scene_info())
-            _, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+            out = torch.empty((fr.plane.ResolutionY, fr.plane.ResolutionX, 4), dtype=torch.float32, device="cuda")
+            st = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr), out.data_ptr(), out.numel() * 4)
             times.append(st.kernel_ms)
         print(json.dumps({"config": f"C5i ({a.instanced} instanced cubes, 1080p 4spp depth 8)",
                           "build": "device extraction + lbvh_gpu_bvh4",

@@ -5,7 +5,8 @@
 // Linear BVH (Karras 2012) built entirely on the GPU:
 //   1. per rank: the primitive's reference record (v0, edge1, edge2 / centre,
 //      r^2), its shading record, its padded bounds and a 64-bit key
-//      30-bit Morton code of the centroid << 32 | (mesh id + 1);
+//      30-bit Morton code of the mesh centre (or the primitive's own centroid)
+//      | mesh id + 1 | Morton code of the centroid inside its mesh's AABB;
 //   2. radix sort of (key, rank) (hipCUB);
 //   3. leaf-order primitive arrays + inline leaf refs (one primitive per leaf,
 //      so leaves are trivially homogeneous in kind and mesh gate);
@@ -46,7 +47,9 @@ struct LbvhInput {
     const int *loose_mat;             // nl
     float scene_lo[3], scene_hi[3];   // Scene.AABB (quantisation box)
     float pad_abs;                    // same padding as the host builder
-    int key_bits;                     // 62 (30-bit Morton above a 32-bit mesh id)
+    const rtd::MeshGate *gates;       // mesh_count exact mesh AABBs (Mesh.AABB, the gates)
+    int mesh_bits;                    // bits of (mesh id + 1) in the sort key
+    int key_bits;                     // 64: 30-bit Morton | mesh id + 1 | in-mesh Morton
 };
 
 struct LbvhOutput {

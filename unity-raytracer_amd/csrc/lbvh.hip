@@ -27,16 +27,16 @@ __device__ __forceinline__ unsigned expand_bits(unsigned v) {
     return v;
 }
 
-__device__ __forceinline__ unsigned morton30(f3 c, const LbvhInput &in) {
+// Morton code of c quantised to `bits` (<= 10) bits per axis inside [lo, hi].
+__device__ __forceinline__ unsigned morton(f3 c, const float lo[3], const float hi[3], int bits) {
     unsigned q[3];
-    const float lo[3] = {in.scene_lo[0], in.scene_lo[1], in.scene_lo[2]};
-    const float hi[3] = {in.scene_hi[0], in.scene_hi[1], in.scene_hi[2]};
     const float cv[3] = {c.x, c.y, c.z};
+    const float cells = (float)(1u << bits);
     for (int a = 0; a < 3; ++a) {
         const float ext = hi[a] - lo[a];
         float t = ext > 0.0f ? (cv[a] - lo[a]) / ext : 0.5f;
         t = fminf(fmaxf(t, 0.0f), 1.0f);
-        q[a] = (unsigned)fminf(t * 1024.0f, 1023.0f);
+        q[a] = (unsigned)fminf(t * cells, cells - 1.0f);
     }
     return (expand_bits(q[0]) << 2) | (expand_bits(q[1]) << 1) | expand_bits(q[2]);
 }
@@ -111,10 +111,27 @@ __global__ void k_prims(LbvhInput in, LbvhOutput out, int n, float4 *plo, float4
     }
     plo[r] = make_float4(lo[0], lo[1], lo[2], 0.0f);
     phi[r] = make_float4(hi[0], hi[1], hi[2], 0.0f);
-    // Spatial order first; the mesh id only breaks ties so that a mesh's
-    // triangles in one Morton cell stay adjacent (mesh-major keys would put
-    // spatially scattered meshes side by side at the top of the tree).
-    keys[r] = ((unsigned long long)morton30(mk(cen[0], cen[1], cen[2]), in) << 32) | (unsigned)(gate + 1);
+    // Two-level key: 30-bit Morton code in the scene box of the mesh's centre
+    // (a loose triangle's or sphere's own centroid) | mesh id + 1 | Morton
+    // code of the centroid inside the mesh's own AABB.  A mesh's triangles
+    // stay contiguous (its subtree carries one exact mesh gate, Scene.cs:67,
+    // and its small pieces collapse into multi-primitive leaves) while meshes
+    // and loose primitives are still ordered spatially at the top.
+    const f3 c = mk(cen[0], cen[1], cen[2]);
+    unsigned long long key;
+    if (gate >= 0) {
+        const rtd::MeshGate g = in.gates[gate];
+        const float mlo[3] = {g.lo.x, g.lo.y, g.lo.z}, mhi[3] = {g.hi.x, g.hi.y, g.hi.z};
+        const f3 mc = mk(0.5f * (mlo[0] + mhi[0]), 0.5f * (mlo[1] + mhi[1]), 0.5f * (mlo[2] + mhi[2]));
+        const int low_bits = 34 - in.mesh_bits;
+        const int per_axis = low_bits >= 30 ? 10 : low_bits / 3;
+        const unsigned long long low = per_axis > 0 ? morton(c, mlo, mhi, per_axis) : 0ull;
+        key = ((unsigned long long)morton(mc, in.scene_lo, in.scene_hi, 10) << 34) |
+              ((unsigned long long)(gate + 1) << low_bits) | low;
+    } else {
+        key = (unsigned long long)morton(c, in.scene_lo, in.scene_hi, 10) << 34;
+    }
+    keys[r] = key;
     vals[r] = r;
 }
 

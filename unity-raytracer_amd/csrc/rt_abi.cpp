@@ -608,8 +608,12 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         ls->valid = false;
     }
     if (ls->scene != ctx->scene_version) {
+        // a new or updated scene (rt_update_mesh_transforms every Update): the
+        // last order stays a valid permutation of the tiles and, animation being
+        // temporally coherent, a good one — keep dispatching by it and measure
+        // this frame's costs for the next
         ls->scene = ctx->scene_version;
-        ls->valid = false;
+        ls->frames = 0;
     }
     if (!ls->valid) ls->frames = 0;
     F.tile_order = ls->valid ? (const int *)ls->order.p : nullptr;
@@ -922,7 +926,10 @@ int set_scene_lbvh(rt_ctx *ctx, const rt_scene_desc *sc, int MT, int NS, int NL,
     in.scene_lo[0] = smin.x; in.scene_lo[1] = smin.y; in.scene_lo[2] = smin.z;
     in.scene_hi[0] = smax.x; in.scene_hi[1] = smax.y; in.scene_hi[2] = smax.z;
     in.pad_abs = pad_abs;
-    in.key_bits = 62;
+    in.gates = (const rtd::MeshGate *)ctx->arr.gates;
+    in.mesh_bits = 0;
+    while ((1ll << in.mesh_bits) <= (long long)sc->mesh_count) ++in.mesh_bits;  // ids 0 .. mesh_count
+    in.key_bits = 64;
     return run_lbvh(ctx, in, wide, S, nodes_count);
 }
 
@@ -1483,6 +1490,7 @@ int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geo
         lights[l].intensity = make_float4(L.intensity.x, L.intensity.y, L.intensity.z, 0.0f);
     }
 
+    HIP_OR_FAIL(ctx, upload(&ctx->arr.gates, gates));  // before the build: the LBVH keys use the mesh boxes
     rtd::SceneDev &S = ctx->S;
     int nodes_count = 0;
     if ((build == RT_BUILD_LBVH_GPU || build == RT_BUILD_LBVH_GPU_BVH2) && P > 0) {
@@ -1599,7 +1607,6 @@ int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geo
     }
     HIP_OR_FAIL(ctx, upload(&ctx->arr.mats, mats));
     HIP_OR_FAIL(ctx, upload(&ctx->arr.lights, lights));
-    HIP_OR_FAIL(ctx, upload(&ctx->arr.gates, gates));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
 
     S.leaves = nullptr;
