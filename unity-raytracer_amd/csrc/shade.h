@@ -124,11 +124,14 @@ __device__ __forceinline__ void reflect(const Surface &s, f3 &o, f3 &d) {
 
 // Primary ray of sample (px, gy, sub-sample s): CastPixelRays :291-298 with
 // n*n stratified offsets ((i + 0.5) / n; n == 1 gives the reference's 0.5).
+// Q4: the frame is 2x2 spp in 4x4-pixel tiles (the bench configurations):
+// the lane -> sample split is shifts, and (i + 0.5) / 2 is an exact halving.
+template <bool Q4 = false>
 __device__ __forceinline__ void primary_ray(const rtd::FrameDev &F, int px, int gy, int s, f3 &o, f3 &d) {
-    const int n = F.spp_n;
-    const int sj = s / n, si = s - sj * n;
-    const float ox = ((float)si + 0.5f) / (float)n;
-    const float oy = ((float)sj + 0.5f) / (float)n;
+    const int n = Q4 ? 2 : F.spp_n;
+    const int sj = Q4 ? s >> 1 : s / n, si = Q4 ? s & 1 : s - sj * n;
+    const float ox = Q4 ? ((float)si + 0.5f) * 0.5f : ((float)si + 0.5f) / (float)n;
+    const float oy = Q4 ? ((float)sj + 0.5f) * 0.5f : ((float)sj + 0.5f) / (float)n;
     const float rm = (((float)px + ox) * F.hl) / (float)F.res_x;
     const float dm = (((float)gy + oy) * F.vl) / (float)F.res_y;
     const f3 pp = (rtt::ld3(F.top_left) + rm * rtt::ld3(F.right)) - rtt::ld3(F.up) * dm;
@@ -191,22 +194,23 @@ __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, 
 
 // Slot (tile, lane) -> pixel; false for lanes outside the image/shard.  A
 // pixel's samples sit in consecutive lanes.
+template <bool Q4 = false>
 __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int lane, int &px, int &ly, int &gy,
                                            int &s) {
-    const int spp = F.spp;
-    const int lp = lane / spp;
+    const int spp = Q4 ? 4 : F.spp;
+    const int lp = Q4 ? lane >> 2 : lane / spp;
     const int pix = lp;
-    s = lane - lp * spp;
+    s = Q4 ? lane & 3 : lane - lp * spp;
+    const int tw = Q4 ? 4 : F.tile_w, th = Q4 ? 4 : F.tile_h;
     const int tx = tile % F.tiles_x, ty = tile / F.tiles_x;
-    px = tx * F.tile_w + pix % F.tile_w;
-    ly = ty * F.tile_h + pix / F.tile_w;
+    px = tx * tw + (Q4 ? pix & 3 : pix % tw);
+    ly = ty * th + (Q4 ? pix >> 2 : pix / tw);
     gy = ly + F.row0;
     if (F.band_count > 1) {
         const int blk = ly / F.band_rows;
         gy = (blk * F.band_count + F.band_index) * F.band_rows + (ly - blk * F.band_rows);
     }
-    return lp < rtd::kWaveSize / spp && pix < F.tile_w * F.tile_h && px < F.res_x && ly < F.local_rows &&
-           gy < F.res_y;
+    return lp < rtd::kWaveSize / spp && pix < tw * th && px < F.res_x && ly < F.local_rows && gy < F.res_y;
 }
 
 }  // namespace rts

@@ -278,16 +278,17 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
 // one of the four (pshift 4: 16 lanes) or sixteen (pshift 2: 4 lanes) waves
 // an expensive tile is split into.
-template <bool COUNT, bool DEEP>
+template <bool COUNT, bool DEEP, bool Q4>
 __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
                                             SegClock &sg) {
     int px, ly, gy, s;
-    const bool active = rts::slot_pixel(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
+    const bool active =
+        rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
     f3 color = mk(0.0f, 0.0f, 0.0f);
     if (active) {
         f3 o, d;
-        rts::primary_ray(F, px, gy, s, o, d);
+        rts::primary_ray<Q4>(F, px, gy, s, o, d);
         cnt.primary += 1;
         if (COUNT) {  // trivially cheap camera samples: they miss Scene.AABB (Scene.cs:54)
             rtt::RayCtx rg;
@@ -301,7 +302,8 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     // rather than kept live across the trace, where it would be spilled
     int tile2 = __builtin_amdgcn_readfirstlane(tile);
     asm volatile("" : "+s"(tile2));
-    const bool active2 = rts::slot_pixel(F, tile2, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
+    const bool active2 =
+        rts::slot_pixel<Q4>(F, tile2, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
     if (active2 && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
@@ -311,8 +313,9 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
 
 // SPLIT: the variant launched when a frame splits tiles (a separate instance, so
 // the common kernel's code and register allocation stay as they are); DEEP:
-// the one for MaxReflectionBounces > kMaxBounces (deep_chain).
-template <bool COUNT, bool SPLIT = false, bool DEEP = false>
+// the one for MaxReflectionBounces > kMaxBounces (deep_chain); Q4: frames of
+// 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel).
+template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false>
 __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
     constexpr bool kPackets = RT_MK_PACKET_SHADOW || RT_MK_PACKET_PRIMARY;
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    render_tile<COUNT, DEEP>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
 #ifdef RT_SEG_PROFILE
     if (!COUNT) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -536,6 +539,9 @@ namespace rtk {
 #ifndef RT_MK_LEVELS
 #define RT_MK_LEVELS 1
 #endif
+#ifndef RT_MK_Q4
+#define RT_MK_Q4 1
+#endif
 // all-packet levels pay off where a wave's tile is small on screen (its
 // mirror rays stay coherent): 16+ samples per pixel = at most 2x2 pixels
 #ifndef RT_MK_LEVELS_MIN_SPP
@@ -546,6 +552,7 @@ namespace rtk {
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
     const int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
+    const bool q4 = RT_MK_Q4 && F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)
             hipLaunchKernelGGL((render_kernel<true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
@@ -553,10 +560,14 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
             hipLaunchKernelGGL((render_kernel<false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     } else if (count_tests)
         hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+    else if ((F.split_tiles > 0 || F.split16_tiles > 0) && q4)
+        hipLaunchKernelGGL((render_kernel<false, true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (F.split_tiles > 0 || F.split16_tiles > 0)
         hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (RT_MK_LEVELS && S.bvh4 && F.spp >= RT_MK_LEVELS_MIN_SPP)
         return launch_render_levels(S, F, stream);
+    else if (q4)
+        hipLaunchKernelGGL((render_kernel<false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     return hipGetLastError();
