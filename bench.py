@@ -153,8 +153,9 @@ def cpu_baseline(rt, fr, budget_s):
     pixels of the same frame: 1 thread (the reference is single-threaded
     Mono) for budget_s, then OpenMP over every host core this job is given
     (the affinity mask, capped by OMP_NUM_THREADS: the GPU box grants a
-    one-GPU job 16 cores of a larger machine) for budget_s / 3.  Mrays/s with
-    the same ray accounting as the GPU line."""
+    one-GPU job 16 cores of a larger machine) for budget_s / 3, then the same
+    threads with a CPU BVH for budget_s / 3.  Mrays/s with the same ray
+    accounting as the GPU line."""
     orc = _rt_pkg.load_oracle()
     rng = np.random.default_rng(20250101)
     total = fr.plane.ResolutionX * fr.plane.ResolutionY
@@ -178,6 +179,19 @@ def cpu_baseline(rt, fr, budget_s):
         msecs += time.perf_counter() - t0
         mrays += c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
         mpix += len(idx)
+    # the same pixels' closest hits through a CPU BVH (oracle BVH mode, equal
+    # answers): the algorithmic part of the GPU's speed-up, separated from
+    # the hardware part; tree build outside the timing
+    bvh = orc.BvhScene(fr)
+    brays, bsecs, bpix = 0, 0.0, 0
+    while bsecs < budget_s / 3:
+        idx = rng.integers(0, total, 64 * threads).astype(np.int32)
+        t0 = time.perf_counter()
+        _, c = bvh.render_pixels(idx, threads=threads)
+        bsecs += time.perf_counter() - t0
+        brays += c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
+        bpix += len(idx)
+    bvh.close()
     return {
         "value": rays / secs / 1e6,
         "unit": "Mrays/s",
@@ -189,6 +203,10 @@ def cpu_baseline(rt, fr, budget_s):
         "all_cores_value": mrays / msecs / 1e6,
         "all_cores_threads": threads,
         "all_cores_sample": f"{mpix} seeded random pixels, {mrays} rays in {msecs:.1f} s",
+        "bvh_all_cores_value": brays / bsecs / 1e6,
+        "bvh_all_cores_sample": f"{bpix} seeded random pixels, {brays} rays in {bsecs:.1f} s, the oracle with a "
+                                f"CPU BVH (median split, leaves <= 4; same answers as the scan), "
+                                f"{threads} threads",
         **facts,
     }
 

@@ -61,6 +61,11 @@ def lib():
         L.orc_render_rows.argtypes = [P, P, P, P, C.c_int32, C.c_int32, P, P, C.c_int32]
         L.orc_render.argtypes = [P, P, P, P, P, P, C.c_int32]
         L.orc_spec_backfacing.argtypes = [C.c_float]
+        L.orc_bvh_build.argtypes = [P]
+        L.orc_bvh_build.restype = P
+        L.orc_bvh_free.argtypes = [P]
+        L.orc_bvh_free.restype = None
+        L.orc_render_pixels_bvh.argtypes = [P, P, P, P, P, P, C.c_int32, P, P, C.c_int32]
         _lib = L
     return _lib
 
@@ -144,6 +149,39 @@ def render_pixels(fr, pixel_indices, threads: int = 0, spp=None):
     if st != 0:
         raise RuntimeError(f"oracle render failed: {st}")
     return out, cnt.as_dict()
+
+
+class BvhScene:
+    """A scene with a CPU BVH over it (CPU-baseline only: the same closest hits
+    as the brute-force scan, found through a tree).  Keeps the descriptor and
+    the tree alive; build time is spent here, outside any render timing."""
+
+    def __init__(self, fr):
+        self.fr = fr
+        self.desc = fr.scene.to_desc()
+        self.h = lib().orc_bvh_build(C.cast(self.desc.ref(), C.c_void_p))
+        if not self.h:
+            raise RuntimeError("oracle BVH build failed")
+
+    def render_pixels(self, pixel_indices, threads: int = 0, spp=None):
+        cam, pl, prm = _frame_structs(self.fr, spp)
+        idx = np.ascontiguousarray(pixel_indices, np.int32)
+        out = np.zeros((len(idx), 4), np.float32)
+        cnt = orc_counts()
+        st = lib().orc_render_pixels_bvh(self.h, C.cast(self.desc.ref(), C.c_void_p), C.byref(cam), C.byref(pl),
+                                         C.byref(prm), _p(idx), len(idx), _p(out), C.byref(cnt),
+                                         threads or default_threads())
+        if st != 0:
+            raise RuntimeError(f"oracle render failed: {st}")
+        return out, cnt.as_dict()
+
+    def close(self):
+        if self.h:
+            lib().orc_bvh_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 def render_rows(fr, row_start, row_step, threads: int = 0, spp=None):

@@ -211,12 +211,222 @@ typedef struct orc_counts {
     uint64_t box_tests, triangle_tests, sphere_tests, shading_fetches;
 } orc_counts;
 
+/* ------------------------------------------------------------------------
+ * Optional CPU BVH for the closest-hit query (CPU-baseline only: separates
+ * the algorithmic speed-up of a BVH from the GPU's).  Same answer as the
+ * brute-force scan: the exact scene and per-mesh AABB gates, padded node
+ * boxes that never cull a primitive the exact tests accept, ties to the
+ * lowest reference rank (meshes, then spheres, then loose triangles, each in
+ * order) — which is the scan's strict-'>' first-wins rule.
+ * --------------------------------------------------------------------- */
+typedef struct {
+    float lo[3], hi[3];
+    int first, count; /* count > 0: leaf over prim[first .. first+count); else children first, first+1 */
+} bnode;
+
+typedef struct orc_bvh {
+    int n, nnodes, mesh_count, mt, ns;
+    int *prim;        /* ranks in leaf order */
+    int *mesh_of;     /* rank -> mesh (mesh triangles) */
+    float *plo, *phi; /* padded bounds per rank */
+    bnode *nodes;
+} orc_bvh;
+
+static const float *g_sort_c;  /* build-time comparator state (single-threaded build) */
+static int g_sort_axis;
+static int cmp_centroid(const void *a, const void *b) {
+    const float ca = g_sort_c[3 * *(const int *)a + g_sort_axis], cb = g_sort_c[3 * *(const int *)b + g_sort_axis];
+    if (ca < cb) return -1;
+    if (ca > cb) return 1;
+    return *(const int *)a - *(const int *)b;
+}
+
+static int bvh_build_rec(orc_bvh *B, const float *cen, int first, int count, int node) {
+    bnode *nd = &B->nodes[node];
+    for (int a = 0; a < 3; ++a) { nd->lo[a] = INFINITY; nd->hi[a] = -INFINITY; }
+    float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = first; i < first + count; ++i) {
+        const int r = B->prim[i];
+        for (int a = 0; a < 3; ++a) {
+            nd->lo[a] = fminf(nd->lo[a], B->plo[3 * r + a]);
+            nd->hi[a] = fmaxf(nd->hi[a], B->phi[3 * r + a]);
+            clo[a] = fminf(clo[a], cen[3 * r + a]);
+            chi[a] = fmaxf(chi[a], cen[3 * r + a]);
+        }
+    }
+    if (count <= 4) {
+        nd->first = first;
+        nd->count = count;
+        return node + 1;
+    }
+    int axis = 0;
+    for (int a = 1; a < 3; ++a)
+        if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+    g_sort_c = cen;
+    g_sort_axis = axis;
+    qsort(B->prim + first, (size_t)count, sizeof(int), cmp_centroid);
+    const int half = count / 2, left = node + 1;
+    const int right = bvh_build_rec(B, cen, first, half, left);
+    const int end = bvh_build_rec(B, cen, first + half, count - half, right);
+    /* children stored as (left, right) indices: left = node + 1 always */
+    nd = &B->nodes[node];
+    nd->first = right;
+    nd->count = 0;
+    return end;
+}
+
+void *orc_bvh_build(const rt_scene_desc *sc) {
+    orc_bvh *B = (orc_bvh *)calloc(1, sizeof *B);
+    if (!B) return NULL;
+    B->mt = sc->mesh_triangle_total;
+    B->ns = sc->sphere_count;
+    B->n = B->mt + B->ns + sc->triangle_count;
+    B->mesh_count = sc->mesh_count;
+    const int n = B->n > 0 ? B->n : 1;
+    B->prim = (int *)malloc(sizeof(int) * (size_t)n);
+    B->mesh_of = (int *)malloc(sizeof(int) * (size_t)n);
+    B->plo = (float *)malloc(sizeof(float) * 3 * (size_t)n);
+    B->phi = (float *)malloc(sizeof(float) * 3 * (size_t)n);
+    float *cen = (float *)malloc(sizeof(float) * 3 * (size_t)n);
+    B->nodes = (bnode *)malloc(sizeof(bnode) * 2 * (size_t)n);
+    rt_aabb box;
+    orc_scene_aabb(sc, &box);
+    float scale = 0.0f;
+    for (int a = 0; a < 3; ++a) scale = fmaxf(scale, fabsf(comp(box.min, a)) + fabsf(comp(box.max, a)));
+    const float pad_abs = ldexpf(fmaxf(scale, 1e-30f), -13);
+    for (int m = 0; m < sc->mesh_count; ++m)
+        for (int i = 0; i < sc->meshes[m].triangle_count; ++i) B->mesh_of[sc->meshes[m].first_triangle + i] = m;
+    for (int r = 0; r < B->n; ++r) {
+        float lo[3], hi[3];
+        if (r >= B->mt && r < B->mt + B->ns) {
+            const rt_sphere sp = sc->spheres[r - B->mt];
+            const float rad = sqrtf(sp.radius_squared);
+            for (int a = 0; a < 3; ++a) { lo[a] = comp(sp.center, a) - rad; hi[a] = comp(sp.center, a) + rad; }
+        } else {
+            const rt_triangle t = r < B->mt ? sc->mesh_triangles[r] : sc->triangles[r - B->mt - B->ns];
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = fminf(comp(t.vertex0, a), fminf(comp(t.vertex1, a), comp(t.vertex2, a)));
+                hi[a] = fmaxf(comp(t.vertex0, a), fmaxf(comp(t.vertex1, a), comp(t.vertex2, a)));
+            }
+        }
+        float ext = 0.0f;
+        for (int a = 0; a < 3; ++a) ext = fmaxf(ext, hi[a] - lo[a]);
+        const float pad = pad_abs + ext * 1e-4f;
+        for (int a = 0; a < 3; ++a) {
+            cen[3 * r + a] = 0.5f * (lo[a] + hi[a]);
+            B->plo[3 * r + a] = lo[a] - pad;
+            B->phi[3 * r + a] = hi[a] + pad;
+        }
+        B->prim[r] = r;
+    }
+    B->nnodes = B->n > 0 ? bvh_build_rec(B, cen, 0, B->n, 0) : 0;
+    free(cen);
+    return B;
+}
+
+void orc_bvh_free(void *h) {
+    orc_bvh *B = (orc_bvh *)h;
+    if (!B) return;
+    free(B->prim); free(B->mesh_of); free(B->plo); free(B->phi); free(B->nodes);
+    free(B);
+}
+
+/* per-thread mesh-gate cache: gate[m] holds (ray stamp << 1 | result) */
+static _Thread_local unsigned long long *t_gate;
+static _Thread_local int t_gate_n;
+static _Thread_local unsigned long long t_stamp;
+
+static rt_hit bvh_intersect(const orc_bvh *B, const rt_scene_desc *sc, const rt_aabb *scene_box,
+                            const rt_ray *ray, orc_tests *ct) {
+    rt_hit hit;
+    hit.type = 0; hit.index = -1; hit.mesh_index = -1;
+    hit.distance = FLT_MAX;
+    ct->box++;
+    if (B->n == 0 || !orc_ray_aabb(ray, scene_box)) return hit; /* Scene.cs:54 */
+    if (t_gate_n < B->mesh_count) {
+        free(t_gate);
+        t_gate = (unsigned long long *)calloc((size_t)B->mesh_count, sizeof *t_gate);
+        t_gate_n = B->mesh_count;
+    }
+    const unsigned long long stamp = ++t_stamp;
+    const float o[3] = {ray->origin.x, ray->origin.y, ray->origin.z};
+    const float inv[3] = {1.0f / ray->direction.x, 1.0f / ray->direction.y, 1.0f / ray->direction.z};
+    float best = FLT_MAX;
+    int best_rank = 0x7fffffff;
+    int stack[128];
+    int sp = 0;
+    int node = 0;
+    for (;;) {
+        const bnode *nd = &B->nodes[node];
+        float tn = 0.0f, tf = INFINITY;
+        for (int a = 0; a < 3; ++a) { /* conservative slab (padded box); NaN operands ignored */
+            const float t1 = (nd->lo[a] - o[a]) * inv[a], t2 = (nd->hi[a] - o[a]) * inv[a];
+            tn = fmaxf(tn, fminf(t1, t2));
+            tf = fminf(tf, fmaxf(t1, t2));
+        }
+        const int enter = tn <= tf && tn <= best;
+        if (enter && nd->count > 0) {
+            for (int i = nd->first; i < nd->first + nd->count; ++i) {
+                const int r = B->prim[i];
+                float t;
+                int ok;
+                if (r < B->mt) {
+                    const int m = B->mesh_of[r];
+                    unsigned long long g = t_gate[m];
+                    if ((g >> 1) != stamp) { /* Mesh.AABB gate, Scene.cs:67, once per ray and mesh */
+                        ct->box++;
+                        g = (stamp << 1) | (unsigned long long)(orc_ray_aabb(ray, &sc->meshes[m].aabb) != 0);
+                        t_gate[m] = g;
+                    }
+                    if (!(g & 1)) continue;
+                    ct->tri++;
+                    ok = orc_ray_triangle(ray, &sc->mesh_triangles[r], &t);
+                } else if (r < B->mt + B->ns) {
+                    ct->sph++;
+                    ok = orc_ray_sphere(ray, &sc->spheres[r - B->mt], &t);
+                } else {
+                    ct->tri++;
+                    ok = orc_ray_triangle(ray, &sc->triangles[r - B->mt - B->ns], &t);
+                }
+                if (ok && (t < best || (t == best && r < best_rank))) {
+                    best = t;
+                    best_rank = r;
+                }
+            }
+        } else if (enter) {
+            stack[sp++] = nd->first; /* right child after the left (node + 1) */
+            node = node + 1;
+            continue;
+        }
+        if (sp == 0) break;
+        node = stack[--sp];
+    }
+    if (best_rank != 0x7fffffff) {
+        hit.distance = best;
+        if (best_rank < B->mt) {
+            const int m = B->mesh_of[best_rank];
+            hit.type = 3; hit.mesh_index = m; hit.index = best_rank - sc->meshes[m].first_triangle;
+        } else if (best_rank < B->mt + B->ns) {
+            hit.type = 1; hit.index = best_rank - B->mt;
+        } else {
+            hit.type = 2; hit.index = best_rank - B->mt - B->ns;
+        }
+    }
+    return hit;
+}
+
 typedef struct {
     const rt_scene_desc *sc;
     rt_aabb scene_box;
     f3 bg255;          /* new Rgb(BackgroundColor) = float3(r,g,b) * 255f, Rgb.cs:15-18 */
     int max_bounces;
+    const orc_bvh *bvh; /* null: the reference's brute-force scan */
 } frame_t;
+
+static rt_hit trace(const frame_t *fr, const rt_ray *ray, orc_tests *ct) {
+    return fr->bvh ? bvh_intersect(fr->bvh, fr->sc, &fr->scene_box, ray, ct)
+                   : intersect(fr->sc, &fr->scene_box, ray, ct);
+}
 
 /* RayTracingSetup.CalculateSpecular, :375-400 */
 static f3 calc_specular(f3 light_dir, f3 ray_dir, f3 n, f3 ks, f3 irr, float phong) {
@@ -232,7 +442,7 @@ static f3 calc_specular(f3 light_dir, f3 ray_dir, f3 n, f3 ks, f3 irr, float pho
 /* RayTracingSetup.Shade, :304-366 (literal recursion) */
 static f3 shade(const frame_t *fr, rt_ray ray, int bounce, orc_counts *cnt) {
     orc_tests ct = {0, 0, 0};
-    rt_hit hit = intersect(fr->sc, &fr->scene_box, &ray, &ct);
+    rt_hit hit = trace(fr, &ray, &ct);
     if (hit.type == 0) {
         cnt->box_tests += ct.box; cnt->triangle_tests += ct.tri; cnt->sphere_tests += ct.sph;
         return fr->bg255;
@@ -264,7 +474,7 @@ static f3 shade(const frame_t *fr, rt_ray ray, int bounce, orc_counts *cnt) {
         rt_ray shadow;
         shadow.origin = add(p, muls(n, SHADOW_RAY_EPSILON));
         shadow.direction = light_dir;
-        rt_hit sh = intersect(sc, &fr->scene_box, &shadow, &ct);
+        rt_hit sh = trace(fr, &shadow, &ct);
         cnt->shadow_rays++;
         float light_dist_sq = distancesq(p, pl->position);
         if (sh.type != 0) {
@@ -334,6 +544,7 @@ static int setup(frame_t *fr, const rt_scene_desc *sc, const rt_image_plane *pla
     int n = isqrt_exact(prm->samples_per_pixel);
     if (n < 0) return RT_E_INVALID;
     fr->sc = sc;
+    fr->bvh = NULL;
     orc_scene_aabb(sc, &fr->scene_box);
     fr->bg255 = muls(V(prm->background_color[0], prm->background_color[1], prm->background_color[2]), 255.0f);
     fr->max_bounces = prm->max_reflection_bounces;
@@ -350,13 +561,31 @@ static f3 top_left_of(const rt_camera *cam, const rt_image_plane *plane) {
 }
 
 /* Render the pixels listed in pix_idx (x + y*res_x) into out (4 floats each). */
+static int render_pixels(const orc_bvh *bvh, const rt_scene_desc *sc, const rt_camera *cam,
+                         const rt_image_plane *plane, const rt_render_params *prm, const int32_t *pix_idx,
+                         int32_t npix, float *out, orc_counts *counts, int32_t threads);
+
 int orc_render_pixels(const rt_scene_desc *sc, const rt_camera *cam, const rt_image_plane *plane,
                       const rt_render_params *prm, const int32_t *pix_idx, int32_t npix,
                       float *out, orc_counts *counts, int32_t threads) {
+    return render_pixels(NULL, sc, cam, plane, prm, pix_idx, npix, out, counts, threads);
+}
+
+/* The same pixels with closest hits through a CPU BVH (orc_bvh_build over sc). */
+int orc_render_pixels_bvh(const void *bvh, const rt_scene_desc *sc, const rt_camera *cam,
+                          const rt_image_plane *plane, const rt_render_params *prm, const int32_t *pix_idx,
+                          int32_t npix, float *out, orc_counts *counts, int32_t threads) {
+    return render_pixels((const orc_bvh *)bvh, sc, cam, plane, prm, pix_idx, npix, out, counts, threads);
+}
+
+static int render_pixels(const orc_bvh *bvh, const rt_scene_desc *sc, const rt_camera *cam,
+                         const rt_image_plane *plane, const rt_render_params *prm, const int32_t *pix_idx,
+                         int32_t npix, float *out, orc_counts *counts, int32_t threads) {
     frame_t fr;
     int n;
     int st = setup(&fr, sc, plane, prm, &n);
     if (st) return st;
+    fr.bvh = bvh;
     f3 tl = top_left_of(cam, plane);
     float hl = plane->half_horizontal_length * 2.0f; /* HorizontalLength, ImagePlane.cs:23 */
     float vl = plane->half_vertical_length * 2.0f;

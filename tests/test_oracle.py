@@ -125,3 +125,33 @@ def test_encode_rgba8_known_answers():
     assert np.array_equal(got, want)
     h = npo.encode_rgba16f(c[:1])
     assert h.dtype == np.float16 and h[0, 0] == np.float16(0.5) and h[0, 3] == 1
+
+
+@pytest.mark.parametrize("name,res", [("demo", None), ("C1", (64, 48)), ("C2", (64, 36)), ("C3", (48, 27)),
+                                      ("C5", (32, 18))])
+def test_cpu_bvh_mode_equals_brute_force(orc, rt, name, res):
+    """The CPU-baseline BVH mode (oracle/rt_oracle.c orc_bvh_*) answers like the scan."""
+    fr = rt.make(name)
+    if res:
+        fr = fr.with_resolution(*res)
+    fr = fr.with_(spp=1, max_bounces=min(fr.max_bounces, 3))
+    idx = np.arange(fr.plane.ResolutionX * fr.plane.ResolutionY, dtype=np.int32)
+    ref, rc = orc.render_pixels(fr, idx)
+    b = orc.BvhScene(fr)
+    got, gc = b.render_pixels(idx)
+    b.close()
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert (gc["primary_rays"], gc["shadow_rays"], gc["reflection_rays"]) == \
+        (rc["primary_rays"], rc["shadow_rays"], rc["reflection_rays"])
+
+
+def test_cpu_bvh_mode_fuzz(orc, rt):
+    import test_gpu_fuzz
+    for seed in range(12):
+        fr = test_gpu_fuzz.random_frame(rt, seed, res=(20, 15), spp=1, bounces=seed % 4)
+        idx = np.arange(300, dtype=np.int32)
+        ref, _ = orc.render_pixels(fr, idx)
+        b = orc.BvhScene(fr)
+        got, _ = b.render_pixels(idx)
+        b.close()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), seed
