@@ -297,11 +297,12 @@ def main():
         if dist_on:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             dist.init_process_group("gloo", rank=rank, world_size=world)
-            print(json.dumps({"launch_check": True, "rank": dist.get_rank(), "world": dist.get_world_size()}),
-                  file=sys.stderr, flush=True)
+            # one write per line: both ranks share the launcher's stderr pipe
+            os.write(2, (json.dumps({"launch_check": True, "rank": dist.get_rank(),
+                                     "world": dist.get_world_size()}) + "\n").encode())
             dist.destroy_process_group()
         else:
-            print(json.dumps({"launch_check": True, "rank": 0, "world": 1}), file=sys.stderr, flush=True)
+            os.write(2, (json.dumps({"launch_check": True, "rank": 0, "world": 1}) + "\n").encode())
         return
     if args.in_process:
         return main_in_process(args)

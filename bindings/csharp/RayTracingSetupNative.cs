@@ -11,10 +11,7 @@
 //     (FindObjectsOfType) and, when they change, the scene is re-sent.
 // PixelColors keeps the reference's Color[] (float RGBA, RT_FLAG_OUT default);
 // set OutputRgba8 to receive Color32[] for a Texture2D instead (4x fewer
-// bytes over PCIe).  The output array is allocated once per resolution, held
-// pinned for its lifetime (GCHandle) and registered with the library
-// (rt_register_host_buffer), so each frame streams into it slab by slab while
-// the rest of the frame renders.
+// bytes over PCIe).
 using System;
 using System.Collections.Generic;
 using System.Linq;
@@ -38,7 +35,6 @@ namespace RayTracer.Native
         public RtStats LastStats;
 
         IntPtr _rt;
-        GCHandle _outHandle;                      // pinned + registered output array
         SceneMesh[] _meshes = Array.Empty<SceneMesh>();
         UnityEngine.Mesh[] _sharedMeshes = Array.Empty<UnityEngine.Mesh>();
         RtMatrix[] _matrices = Array.Empty<RtMatrix>();
@@ -52,26 +48,8 @@ namespace RayTracer.Native
 
         void OnDestroy()
         {
-            ReleaseOutput();
             if (_rt != IntPtr.Zero) Rt.rt_destroy(_rt);
             _rt = IntPtr.Zero;
-        }
-
-        // Pins a freshly allocated output array and registers it with the library.
-        void HoldOutput(Array a, int bytesPerPixel)
-        {
-            ReleaseOutput();
-            _outHandle = GCHandle.Alloc(a, GCHandleType.Pinned);
-            var bytes = new UIntPtr((ulong)a.Length * (ulong)bytesPerPixel);
-            if (a.Length > 0 && Rt.rt_register_host_buffer(_rt, _outHandle.AddrOfPinnedObject(), bytes) != Rt.OK)
-                Debug.LogError(Rt.LastError(_rt));  // frames still render, through a copy
-        }
-
-        void ReleaseOutput()
-        {
-            if (!_outHandle.IsAllocated) return;
-            if (_rt != IntPtr.Zero) Rt.rt_unregister_host_buffer(_rt, _outHandle.AddrOfPinnedObject());
-            _outHandle.Free();
         }
 
         void Update()
@@ -201,20 +179,12 @@ namespace RayTracer.Native
             int st;
             if (OutputRgba8)
             {
-                if (PixelColors32.Length != n || !_outHandle.IsAllocated || _outHandle.Target != (object)PixelColors32)
-                {
-                    if (PixelColors32.Length != n) PixelColors32 = new Color32[n];
-                    HoldOutput(PixelColors32, 4);
-                }
+                if (PixelColors32.Length != n) PixelColors32 = new Color32[n];
                 st = Rt.rt_render_rgba8(_rt, ref cameraData, ref plane, ref p, PixelColors32, out LastStats);
             }
             else
             {
-                if (PixelColors.Length != n || !_outHandle.IsAllocated || _outHandle.Target != (object)PixelColors)
-                {
-                    if (PixelColors.Length != n) PixelColors = new Color[n];
-                    HoldOutput(PixelColors, 16);
-                }
+                if (PixelColors.Length != n) PixelColors = new Color[n];
                 st = Rt.rt_render(_rt, ref cameraData, ref plane, ref p, PixelColors, out LastStats);
             }
             if (st != Rt.OK) Debug.LogError(Rt.LastError(_rt));

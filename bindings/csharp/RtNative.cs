@@ -146,8 +146,6 @@ namespace RayTracer.Native
         [DllImport(Lib)] public static extern void rt_destroy(IntPtr ctx);
         [DllImport(Lib)] public static extern IntPtr rt_last_error(IntPtr ctx);
         [DllImport(Lib)] public static extern int rt_set_stream(IntPtr ctx, IntPtr hipStream);
-        [DllImport(Lib)] public static extern int rt_register_host_buffer(IntPtr ctx, IntPtr host, UIntPtr bytes);
-        [DllImport(Lib)] public static extern int rt_unregister_host_buffer(IntPtr ctx, IntPtr host);
         [DllImport(Lib)] public static extern int rt_set_scene(IntPtr ctx, ref RtSceneDesc scene);
         [DllImport(Lib)] public static extern int rt_set_scene_ex(IntPtr ctx, ref RtSceneDesc scene, int build);
         [DllImport(Lib)] public static extern int rt_get_scene_info(IntPtr ctx, out RtSceneInfo info);

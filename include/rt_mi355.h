@@ -256,23 +256,6 @@ const char *rt_last_error(const rt_ctx *ctx);
  * its own work with the library's). */
 int rt_set_stream(rt_ctx *ctx, void *hip_stream);
 
-/* Registers a caller-owned host output buffer until rt_unregister_host_buffer
- * (or rt_destroy): the range is page-locked and mapped into the device's
- * address space.  rt_render frames whose out_rgba lies inside it no longer
- * render-then-copy: one launch dispatches the frame slab by slab (row slabs of
- * ~4 MB, longest-first inside each), and a small copier kernel streams every
- * finished slab over PCIe into the buffer while the rest of the frame renders
- * (frames of other render paths are copied into it after the launch, at the
- * page-locked rate).  The caller keeps the memory allocated — and, from a
- * garbage-collected host, pinned: C# GCHandle.Alloc(PixelColors,
- * GCHandleType.Pinned) — until it unregisters it.  It is how the Color[]
- * PixelColors that CastPixelRays fills every Update (RayTracingSetup.cs:40,
- * 198, 275-302) is handed over once instead of per frame.  Ranges must not
- * overlap. */
-int rt_register_host_buffer(rt_ctx *ctx, void *host, size_t bytes);
-/* Waits for the device, then unlocks a registered buffer. */
-int rt_unregister_host_buffer(rt_ctx *ctx, void *host);
-
 /* Upload a scene: copies every array to HBM, computes Scene.AABB exactly as
  * Scene.CalculateAABB (Scene.cs:17-41) and builds the BVH.  Replaces
  * RayTracingSetup.UpdateScene()'s result (:120-128). */

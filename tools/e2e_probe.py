@@ -48,40 +48,6 @@ def main():
         ks.append(time.perf_counter() - t0)
     out["render_device_ms"] = med(ks)
     out["kernel_ms"] = round(st.kernel_ms, 4)
-    # a registered (page-locked, mapped) host Color[]: the kernels store into it directly
-    host = np.zeros((ry, rx, ch), dt)
-    t0 = time.perf_counter()
-    ctx.register_host_buffer(host)
-    out["register_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
-    ts = []
-    for _ in range(a.frames):
-        t0 = time.perf_counter()
-        _, st = ctx.render(fr.camera, fr.plane, p, out=host)
-        ts.append(time.perf_counter() - t0)
-    out["render_registered_ms"] = med(ts)
-    out["render_registered_kernel_ms"] = round(st.kernel_ms, 4)
-    ref = np.empty_like(host)
-    torch.from_numpy(ref.reshape(-1).view(np.uint8)).copy_(dev.cpu())
-    out["render_registered_equal"] = bool(np.array_equal(ref.view(np.uint32), host.view(np.uint32)))
-    t0 = time.perf_counter()
-    ctx.unregister_host_buffer(host)
-    out["unregister_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
-    # a registered host Color[] (rt_register_host_buffer): slabs stream to it during the frame
-    host = np.zeros((ry, rx, ch), dt)
-    t0 = time.perf_counter()
-    ctx.register_host_buffer(host)
-    out["register_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
-    ts = []
-    for _ in range(a.frames):
-        t0 = time.perf_counter()
-        _, st = ctx.render(fr.camera, fr.plane, p, out=host)
-        ts.append(time.perf_counter() - t0)
-    out["render_registered_ms"] = med(ts)
-    out["render_registered_kernel_ms"] = round(st.kernel_ms, 4)
-    ref = np.empty_like(host)
-    torch.from_numpy(ref.reshape(-1).view(np.uint8)).copy_(dev.cpu())
-    out["render_registered_equal"] = bool(np.array_equal(ref.view(np.uint32), host.view(np.uint32)))
-    ctx.unregister_host_buffer(host)
     for kind in ("pageable", "pinned"):
         if kind == "pinned":
             host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy().view(dt).reshape(ry, rx, ch)

@@ -200,8 +200,6 @@ SIGNATURES = {
     "rt_destroy": (None, [_P]),
     "rt_last_error": (C.c_char_p, [_P]),
     "rt_set_stream": (C.c_int, [_P, _P]),
-    "rt_register_host_buffer": (C.c_int, [_P, _P, C.c_size_t]),
-    "rt_unregister_host_buffer": (C.c_int, [_P, _P]),
     "rt_set_scene": (C.c_int, [_P, C.POINTER(rt_scene_desc)]),
     "rt_set_scene_ex": (C.c_int, [_P, C.POINTER(rt_scene_desc), C.c_int32]),
     "rt_get_scene_info": (C.c_int, [_P, C.POINTER(rt_scene_info)]),

@@ -11,18 +11,10 @@ namespace rtk {
 // One frame (or one row shard of it): CastPixelRays + Shade, RayTracingSetup.cs:275-366.
 // Megakernel: one lane per sample, whole Whitted chain in one launch (trace.hip).
 // Longest-first tile order for the next frame (trace.hip).
-// Keys: 9-bit log cost (descending), above it the slab rank of a
-// registered-host-buffer frame (kProgKeyBits in all).
-constexpr int kCostKeyBits = 9;
-constexpr int kProgKeyBits = 12;
 size_t tile_sort_scratch_bytes(int n);
 hipError_t launch_iota(int *p, int n, hipStream_t stream);
 hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const int *iota, int *order, int n,
-                              int key_bits, void *scratch, size_t scratch_bytes, hipStream_t stream);
-
-// Streams the finished slabs of a registered-host-buffer frame
-// (rtd::Progress) from the device frame to the mapped host buffer.
-hipError_t launch_copier(const rtd::Progress *P, const void *src, void *dst_host, hipStream_t stream);
+                              void *scratch, size_t scratch_bytes, hipStream_t stream);
 
 hipError_t launch_render_mega(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
                               hipStream_t stream);

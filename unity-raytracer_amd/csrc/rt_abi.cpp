@@ -191,18 +191,6 @@ struct rt_ctx {
     std::vector<std::pair<hipStream_t, hipEvent_t>> async_end;
     // rt_render's slab pipeline: copy stream + one event per slab
     hipStream_t copy_stream = nullptr;
-    // host outputs registered with rt_register_host_buffer (page-locked and
-    // mapped; run_frame_registered streams frames into them)
-    struct HostReg {
-        char *host;
-        size_t bytes;
-        char *dev;
-    };
-    std::vector<HostReg> host_regs;
-    GrowBuf progress;         // rtd::Progress of the registered-buffer frames
-    rtd::Progress prog_host;  // its host image (kept: the upload reads it asynchronously)
-    GrowBuf tile_done;        // per-tile completion flags (Progress::tile_done)
-    unsigned prog_seq = 0;
     std::vector<hipEvent_t> slab_done;
     // multi-device context: this context is member 0 (the root, device 0 of
     // the frame); peers[i] is member i + 1, a single-device context of its own
@@ -654,8 +642,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
 
 int lpt_sort_now(rt_ctx *ctx, const rtd::FrameDev &F, LptSlot *ls) {
     HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
-                                             (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
-                                             F.progress ? rtk::kProgKeyBits : rtk::kCostKeyBits, ls->scratch.p,
+                                             (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles, ls->scratch.p,
                                              ls->scratch.cap, ctx->stream));
     ls->valid = true;
     return RT_OK;
@@ -812,89 +799,6 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     return RT_OK;
 }
 
-
-// rt_render into a registered host buffer (device address dev_host): ONE
-// whole-frame megakernel launch dispatched slab-major (tile-row slabs of
-// ~4 MB, longest-first inside each), whose waves write their pixels through to
-// memory and count finished slabs, and copier_kernel on the high-priority copy
-// stream, which streams every finished slab over PCIe into the host buffer
-// while the rest of the frame renders.  Separate slab launches or runtime
-// copies cannot overlap the two on this stack.
-int run_frame_registered(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *host_out,
-                         void *dev_host, size_t out_bytes, rt_stats *stats,
-                         std::chrono::steady_clock::time_point t_start) {
-    Range range("rt_frame_registered");
-    int st = settle_async(ctx);
-    if (st) return st;
-    if (!ctx->copy_stream) {
-        int least = 0, greatest = 0;
-        HIP_OR_FAIL(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_OR_FAIL(ctx, hipStreamCreateWithPriority(&ctx->copy_stream, hipStreamNonBlocking, greatest));
-    }
-    F.out = ctx->d_out;
-    F.counters = ctx->d_counters;
-    const size_t row_bytes = out_bytes / (size_t)F.local_rows;
-    const int tile_rows = (F.local_rows + F.tile_h - 1) / F.tile_h;
-    const int nslab = (int)std::max<size_t>(
-        1, std::min<size_t>({(size_t)rtd::kProgSlabs, (size_t)tile_rows, out_bytes / ((size_t)4 << 20)}));
-    // completion flags, one per tile: grown zeroed, then marked with a new
-    // sequence number by every frame (no per-frame reset)
-    if (ctx->tile_done.cap < (size_t)F.num_tiles * 4) {
-        HIP_OR_FAIL(ctx, ensure(ctx, ctx->tile_done, (size_t)F.num_tiles * 4));
-        HIP_OR_FAIL(ctx, hipMemset(ctx->tile_done.p, 0, ctx->tile_done.cap));
-    }
-    if (++ctx->prog_seq == 0) ++ctx->prog_seq;
-    rtd::Progress &hp = ctx->prog_host;
-    std::memset(&hp, 0, sizeof hp);
-    hp.nslab = nslab;
-    hp.tiles_x = F.tiles_x;
-    hp.seq = ctx->prog_seq;
-    hp.tile_done = (unsigned *)ctx->tile_done.p;
-    for (int k = 0; k < nslab; ++k) {
-        const int r1 = (int)((long long)tile_rows * (k + 1) / nslab);
-        hp.row_end[k] = r1;
-        hp.byte_end[k] = (unsigned long long)std::min(F.local_rows, r1 * F.tile_h) * row_bytes;
-    }
-    HIP_OR_FAIL(ctx, ensure(ctx, ctx->progress, sizeof(rtd::Progress)));
-    rtd::Progress *dp = (rtd::Progress *)ctx->progress.p;
-    F.progress = dp;
-    // longest-first state of its own (slab-major keys, no tile splits)
-    LptSlot *ls = nullptr;
-    bool lpt_sort = false;
-    st = lpt_prepare(ctx, F, prm, true, false, 1000 + nslab, ls, lpt_sort);
-    if (st) return st;
-    F.split_tiles = 0;
-    F.split16_tiles = 0;
-    const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
-    HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes, ctx->stream));
-    HIP_OR_FAIL(ctx, hipMemcpyAsync(dp, &hp, sizeof hp, hipMemcpyHostToDevice, ctx->stream));
-    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, false, ctx->stream));
-    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    // the copier starts after the counters are zeroed, behind the frame's launch
-    HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->copy_stream, ctx->ev0, 0));
-    HIP_OR_FAIL(ctx, rtk::launch_copier(dp, ctx->d_out, dev_host, ctx->copy_stream));
-    if (lpt_sort) {
-        st = lpt_sort_now(ctx, F, ls);
-        if (st) return st;
-    }
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->copy_stream));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
-    int err = 0;
-    HIP_OR_FAIL(ctx, hipMemcpy(&err, &dp->error, sizeof err, hipMemcpyDeviceToHost));
-    if (err)  // the copier gave up waiting (never expected): copy the finished frame here
-        HIP_OR_FAIL(ctx, hipMemcpy(host_out, ctx->d_out, out_bytes, hipMemcpyDeviceToHost));
-    unsigned long long counts[rtd::kCounterWords];
-    st = read_counters(ctx, counts);
-    if (st) return st;
-    if (stats) {
-        float ms = 0.0f;
-        HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-        fill_stats(stats, counts, ms,
-                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
-    }
-    return RT_OK;
-}
 
 // Scene.CalculateAABB (Scene.cs:17-41) with Unity min/max semantics:
 // mesh AABBs, then loose triangle vertices, then sphere boxes.
@@ -1101,11 +1005,6 @@ int create_one(int dev, rt_ctx **out) {
 void destroy_one(rt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
-    for (const auto &r : ctx->host_regs) (void)hipHostUnregister(r.host);
-    ctx->host_regs.clear();
-    if (ctx->progress.p) (void)hipFree(ctx->progress.p);
-    if (ctx->tile_done.p) (void)hipFree(ctx->tile_done.p);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
     free_scene(ctx);
     free_wavefront(ctx);
@@ -1939,14 +1838,6 @@ int32_t rt_band_rows_local(int32_t resolution_y, int32_t band_index, int32_t ban
     return band_local_rows(resolution_y, band_count <= 0 ? 1 : band_count, band_rows <= 0 ? 8 : band_rows);
 }
 
-// Device address of a registered host range holding [host, host + bytes), or null.
-static void *mapped_host(const rt_ctx *ctx, void *host, size_t bytes) {
-    char *h = (char *)host;
-    for (const auto &r : ctx->host_regs)
-        if (h >= r.host && bytes <= r.bytes && (size_t)(h - r.host) <= r.bytes - bytes) return r.dev + (h - r.host);
-    return nullptr;
-}
-
 int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane, const rt_render_params *params,
               void *out_rgba, rt_stats *stats) {
     if (!ctx) return RT_E_INVALID;
@@ -1973,47 +1864,7 @@ int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
     if (bytes && !out_rgba) return fail(ctx, RT_E_INVALID, "out_rgba is null");
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     HIP_OR_FAIL(ctx, ensure_out(ctx, bytes));
-    if (void *mapped = bytes ? mapped_host(ctx, out_rgba, bytes) : nullptr) {
-        // plain megakernel frames stream into the registered buffer; the rest
-        // (counting, deep, levels, other paths) render, then DMA into it
-        const Path P = frame_path(ctx, params);
-        const bool levels = ctx->S.bvh4 && F.spp >= 16;  // the all-packet levels kernel (trace.hip)
-        if (P.mega && !P.count && !levels && F.max_bounces <= rtd::kMaxBounces && F.num_tiles > 0)
-            return run_frame_registered(ctx, F, params, out_rgba, mapped, bytes, stats, t0);
-    }
     return run_frame(ctx, F, params, ctx->d_out, stats, t0, out_rgba, bytes);
-}
-
-int rt_register_host_buffer(rt_ctx *ctx, void *host, size_t bytes) {
-    if (!ctx) return RT_E_INVALID;
-    if (!host || bytes == 0) return fail(ctx, RT_E_INVALID, "null or empty host buffer");
-    for (const auto &r : ctx->host_regs)
-        if ((char *)host < r.host + r.bytes && r.host < (char *)host + bytes)
-            return fail(ctx, RT_E_INVALID, "host buffer overlaps a registered one");
-    DeviceGuard guard;
-    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    HIP_OR_FAIL(ctx, hipHostRegister(host, bytes, hipHostRegisterMapped));
-    void *dev = nullptr;
-    if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess || !dev) {
-        (void)hipHostUnregister(host);
-        return fail(ctx, RT_E_HIP, "hipHostGetDevicePointer failed");
-    }
-    ctx->host_regs.push_back({(char *)host, bytes, (char *)dev});
-    return RT_OK;
-}
-
-int rt_unregister_host_buffer(rt_ctx *ctx, void *host) {
-    if (!ctx) return RT_E_INVALID;
-    for (size_t i = 0; i < ctx->host_regs.size(); ++i) {
-        if (ctx->host_regs[i].host != (char *)host) continue;
-        DeviceGuard guard;
-        HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-        HIP_OR_FAIL(ctx, hipDeviceSynchronize());  // no frame or copy may still write it
-        HIP_OR_FAIL(ctx, hipHostUnregister(host));
-        ctx->host_regs.erase(ctx->host_regs.begin() + (long)i);
-        return RT_OK;
-    }
-    return fail(ctx, RT_E_INVALID, "host buffer %p is not registered", host);
 }
 
 int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,

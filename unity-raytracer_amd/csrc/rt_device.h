@@ -164,24 +164,6 @@ __host__ __device__ __forceinline__ unsigned tile_cost_key(unsigned long long c6
     return e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
 }
 
-// rt_render into a registered host buffer (rt_register_host_buffer): the
-// frame's waves are dispatched slab-major (whole tile-row slabs, each
-// longest-first inside) and mark their tiles finished; a small copier kernel
-// streams every finished slab to the host while the rest of the frame renders.
-// Completion is one flag word per tile (the frame's sequence number, stored
-// through to memory after the tile's pixels) — counters would serialise every
-// wave of a slab on one atomic address.
-constexpr int kProgSlabs = 8;
-struct Progress {
-    int nslab;
-    int tiles_x;
-    int row_end[kProgSlabs];                  // tile-row end of each slab (tiles are row-major)
-    unsigned long long byte_end[kProgSlabs];  // output byte end of each slab
-    unsigned seq;                             // this frame's sequence number (never 0)
-    unsigned *tile_done;                      // num_tiles flags: seq once the tile's pixels are in memory
-    int error;                                // the copier timed out (the host then copies itself)
-};
-
 // Per-frame constants of CastPixelRays (RayTracingSetup.cs:277-284).
 struct FrameDev {
     float cam_pos[3];
@@ -205,7 +187,6 @@ struct FrameDev {
     int split16_tiles;       // render_kernel: the first split16_tiles of tile_order run as 16 sixteenth-waves each,
     int split_tiles;         // ... the next split_tiles as 4 quarter-waves each
     unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
-    Progress *progress;            // slab progress of a registered-host-buffer frame (render_kernel<..., PROG>)
 };
 
 }  // namespace rtd

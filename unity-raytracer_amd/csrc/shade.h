@@ -174,46 +174,10 @@ __device__ __forceinline__ unsigned half_bits(float c) {
     return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)c);  // round to nearest even
 }
 
-// Output words written through to memory (sc1 stores: the line leaves this
-// XCD's L2 for memory), so another XCD's copier can read them once the wave's
-// stores have drained, without an L2 write-back.  One store instruction per
-// pixel; a store has no result register, so the asm needs no wait of its own.
-typedef unsigned v2u __attribute__((ext_vector_type(2)));
-typedef unsigned v3u __attribute__((ext_vector_type(3)));
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store_through(unsigned *p, unsigned v) {
-    asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void store_through2(unsigned *p, unsigned a, unsigned b) {
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v2u{a, b}) : "memory");
-}
-__device__ __forceinline__ void store_through3(unsigned *p, unsigned a, unsigned b, unsigned c) {
-    asm volatile("global_store_dwordx3 %0, %1, off sc1" ::"v"(p), "v"(v3u{a, b, c}) : "memory");
-}
-__device__ __forceinline__ void store_through4(unsigned *p, unsigned a, unsigned b, unsigned c, unsigned d) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v4u{a, b, c, d}) : "memory");
-}
-
 // Final pixel store: v is the sample mean in Rgb.Value units (0..255);
 // Rgb.Color = Value / 255 (Rgb.cs:13), then the requested output format.
-// THROUGH: written through to memory (a registered-host-buffer frame).
-template <bool THROUGH = false>
 __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, rtm::f3 v) {
     const float r = v.x / 255.0f, g = v.y / 255.0f, b = v.z / 255.0f;
-    if (THROUGH) {
-        unsigned *q = (unsigned *)F.out;
-        if (F.out_format == rtd::kOutRGBA8) {
-            store_through(q + idx, encode8(r) | (encode8(g) << 8) | (encode8(b) << 16) | (255u << 24));
-        } else if (F.out_format == rtd::kOutRGB32F) {
-            store_through3(q + idx * 3, __float_as_uint(r), __float_as_uint(g), __float_as_uint(b));
-        } else if (F.out_format == rtd::kOutRGBA16F) {
-            store_through2(q + idx * 2, half_bits(r) | (half_bits(g) << 16), half_bits(b) | (0x3C00u << 16));
-        } else {
-            store_through4(q + idx * 4, __float_as_uint(r), __float_as_uint(g), __float_as_uint(b),
-                           __float_as_uint(1.0f));
-        }
-        return;
-    }
     if (F.out_format == rtd::kOutRGBA8) {
         ((unsigned *)F.out)[idx] = encode8(r) | (encode8(g) << 8) | (encode8(b) << 16) | (255u << 24);
     } else if (F.out_format == rtd::kOutRGB32F) {

@@ -278,7 +278,7 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
 // one of the four (pshift 4: 16 lanes) or sixteen (pshift 2: 4 lanes) waves
 // an expensive tile is split into.
-template <bool COUNT, bool DEEP, bool Q4, bool PROG>
+template <bool COUNT, bool DEEP, bool Q4>
 __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
                                             SegClock &sg) {
@@ -307,17 +307,15 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     if (active2 && s == 0) {
         f3 v = sum;
         if (F.spp > 1) v = v / (float)F.spp;
-        rts::store_pixel<PROG>(F, (size_t)ly * F.res_x + px, v);
+        rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
     }
 }
 
 // SPLIT: the variant launched when a frame splits tiles (a separate instance, so
 // the common kernel's code and register allocation stay as they are); DEEP:
 // the one for MaxReflectionBounces > kMaxBounces (deep_chain); Q4: frames of
-// 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel); PROG: a
-// registered-host-buffer frame (pixels written through, finished slabs
-// reported to rtd::Progress for copier_kernel).
-template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false, bool PROG = false>
+// 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel).
+template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false>
 __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
     constexpr bool kPackets = RT_MK_PACKET_SHADOW || RT_MK_PACKET_PRIMARY;
@@ -353,7 +351,7 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    render_tile<COUNT, DEEP, Q4, PROG>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
 #ifdef RT_SEG_PROFILE
     if (!COUNT) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -384,154 +382,9 @@ __global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(Sce
     }
 #endif
     if (F.tile_cost && lane == 0 && part <= 0) {
-        unsigned key = tile_cost_key(__builtin_amdgcn_s_memtime() - t0, part, pshift);
-        if (PROG) {  // slab-major: the slab rank above the cost (sorted descending)
-            const int row = tile / F.tiles_x;
-            int k = 0;
-            while (k + 1 < F.progress->nslab && row >= F.progress->row_end[k]) ++k;
-            key |= (unsigned)(kProgSlabs - 1 - k) << rtk::kCostKeyBits;
-        }
-        F.tile_cost[tile] = key;
+        F.tile_cost[tile] = tile_cost_key(__builtin_amdgcn_s_memtime() - t0, part, pshift);
     }
     rtt::flush_counts<COUNT>(cnt, F.counters);
-    if (PROG && part <= 0) {
-        // this wave's write-through pixel stores are complete before its tile is marked
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_store(F.progress->tile_done + tile, F.progress->seq, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Streams each finished slab of a registered-host-buffer frame to the host
-// buffer (mapped, so plain stores cross PCIe).  Started after the frame's
-// launch on a high-priority stream: a few waves that take CU slots as the
-// frame's waves free them.  The frame never waits on it, so no ordering
-// between the two launches can deadlock; a poll that outlives kCopierTimeout
-// shader cycles (~2 s) sets P->error and the host copies the frame itself.
-#ifndef RT_COPIER_PIPE
-#define RT_COPIER_PIPE 0
-#endif
-#ifndef RT_COPIER_BLOCKS
-#define RT_COPIER_BLOCKS 64
-#endif
-constexpr int kCopierBlocks = RT_COPIER_BLOCKS;
-constexpr unsigned long long kCopierTimeout = 5000000000ull;
-// sc1 loads (not a stale line of this XCD's L2): four in flight per thread,
-// then one wait that names their registers, so the compiler can neither use a
-// register before its load landed nor reuse one that a load still writes.
-__device__ __forceinline__ void copy4x16(const char *s, char *d, size_t stride) {
-    rts::v4u a, b, c, e;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(a) : "v"(s) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(b) : "v"(s + stride) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(c) : "v"(s + 2 * stride) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(e) : "v"(s + 3 * stride) : "memory");
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(e)::"memory");
-    *(rts::v4u *)d = a;
-    *(rts::v4u *)(d + stride) = b;
-    *(rts::v4u *)(d + 2 * stride) = c;
-    *(rts::v4u *)(d + 3 * stride) = e;
-}
-
-// Bytes [b0, b1) of the frame to the host: dwords up to a `unit`-aligned
-// offset (16: the host buffer shares the device buffer's 16-B alignment), then
-// 16-B units four per thread per step, then the dword tail.
-__device__ __forceinline__ void copy_range(const unsigned *src, unsigned *dst, size_t b0, size_t b1, int unit) {
-    const size_t nthreads = (size_t)gridDim.x * 256, me = (size_t)blockIdx.x * 256 + threadIdx.x;
-    size_t h = b0, t = b1;
-    if (unit == 16) {
-        h = (b0 + 15) & ~(size_t)15;
-        t = b1 & ~(size_t)15;
-        if (h > t) h = t = b1;
-    } else {
-        h = t = b1;
-    }
-    for (size_t i = b0 / 4 + me; i < h / 4; i += nthreads)
-        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const char *s = (const char *)src;
-    char *d = (char *)dst;
-    const size_t units = (t - h) / 16, step = nthreads * 4;
-    size_t u = me;
-#if RT_COPIER_PIPE
-    // software-pipelined: the next batch's loads are issued before this
-    // batch's stores, so a wait for the loads (vmcnt counts in issue order)
-    // leaves the stores to the host in flight
-    if (u + 3 * nthreads < units) {
-        const size_t stride = nthreads * 16;
-        rts::v4u a0, a1, a2, a3;
-        const char *p = s + h + u * 16;
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(a0) : "v"(p) : "memory");
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(a1) : "v"(p + stride) : "memory");
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(a2) : "v"(p + 2 * stride) : "memory");
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(a3) : "v"(p + 3 * stride) : "memory");
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
-        for (;;) {
-            char *q = d + h + u * 16;
-            const size_t un = u + step;
-            if (un + 3 * nthreads < units) {
-                rts::v4u b0, b1, b2, b3;
-                const char *pn = s + h + un * 16;
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(b0) : "v"(pn) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(b1) : "v"(pn + stride) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(b2) : "v"(pn + 2 * stride) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(b3) : "v"(pn + 3 * stride) : "memory");
-                *(rts::v4u *)q = a0;  // plain stores: ordered by the asm's memory clobbers
-                *(rts::v4u *)(q + stride) = a1;
-                *(rts::v4u *)(q + 2 * stride) = a2;
-                *(rts::v4u *)(q + 3 * stride) = a3;
-                asm volatile("s_waitcnt vmcnt(4)" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3)::"memory");
-                a0 = b0; a1 = b1; a2 = b2; a3 = b3;
-                u = un;
-            } else {
-                *(rts::v4u *)q = a0;
-                *(rts::v4u *)(q + stride) = a1;
-                *(rts::v4u *)(q + 2 * stride) = a2;
-                *(rts::v4u *)(q + 3 * stride) = a3;
-                u = un;
-                break;
-            }
-        }
-    }
-#else
-    for (; u + 3 * nthreads < units; u += step) copy4x16(s + h + u * 16, d + h + u * 16, nthreads * 16);
-#endif
-    for (; u < units; u += nthreads) {
-        rts::v4u a;
-        asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(a) : "v"(s + h + u * 16) : "memory");
-        *(rts::v4u *)(d + h + u * 16) = a;
-    }
-    for (size_t i = t / 4 + me; i < b1 / 4; i += nthreads)
-        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(256) void copier_kernel(Progress *P, const unsigned *src, unsigned *dst) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    const int unit = ((unsigned long long)dst & 15) == 0 ? 16 : 4;  // src is 256-B aligned
-    const unsigned seq = P->seq;
-    for (int k = 0; k < P->nslab; ++k) {
-        // every tile of slab k marked with this frame's number; each thread
-        // resumes at its first unfinished flag, so a poll costs one load per
-        // thread, not a rescan of the slab
-        const int t0k = (k ? P->row_end[k - 1] : 0) * P->tiles_x, t1k = P->row_end[k] * P->tiles_x;
-        int timed_out = 0;
-        int cur = t0k + (int)threadIdx.x;
-        while (true) {
-            while (cur < t1k &&
-                   __hip_atomic_load(P->tile_done + cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == seq)
-                cur += 256;
-            if (!__syncthreads_or(cur < t1k)) break;
-            if (__syncthreads_or(__builtin_amdgcn_s_memtime() - t0 > kCopierTimeout)) {  // a block-wide verdict
-                timed_out = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(32);
-        }
-        if (timed_out) {
-            if (threadIdx.x == 0) __hip_atomic_store(&P->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
-        }
-        copy_range(src, dst, k ? P->byte_end[k - 1] : 0ull, P->byte_end[k], unit);
-    }
 }
 
 // Wave-synchronous megakernel: the Whitted chain advances level by level for
@@ -700,15 +553,6 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
     if (F.num_tiles <= 0) return hipSuccess;
     const int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
     const bool q4 = RT_MK_Q4 && F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
-    if (F.progress) {  // the host routes only plain megakernel frames here (no count, split, deep or levels)
-        if (q4)
-            hipLaunchKernelGGL((render_kernel<false, false, false, true, true>), dim3(blocks), dim3(kMkThreads), 0,
-                               stream, S, F);
-        else
-            hipLaunchKernelGGL((render_kernel<false, false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0,
-                               stream, S, F);
-        return hipGetLastError();
-    }
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)
             hipLaunchKernelGGL((render_kernel<true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
@@ -734,14 +578,8 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
 size_t tile_sort_scratch_bytes(int n) {
     size_t bytes = 0;
     (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, bytes, (const unsigned *)nullptr, (unsigned *)nullptr,
-                                                        (const int *)nullptr, (int *)nullptr, n, 0, kProgKeyBits);
+                                                        (const int *)nullptr, (int *)nullptr, n, 0, 9);
     return bytes;
-}
-
-hipError_t launch_copier(const Progress *P, const void *src, void *dst_host, hipStream_t stream) {
-    hipLaunchKernelGGL(copier_kernel, dim3(kCopierBlocks), dim3(256), 0, stream, (Progress *)P, (const unsigned *)src,
-                       (unsigned *)dst_host);
-    return hipGetLastError();
 }
 
 __global__ void iota_kernel(int *p, int n) {
@@ -758,10 +596,10 @@ hipError_t launch_iota(int *p, int n, hipStream_t stream) {
 }
 
 hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const int *iota, int *order, int n,
-                              int key_bits, void *scratch, size_t scratch_bytes, hipStream_t stream) {
+                              void *scratch, size_t scratch_bytes, hipStream_t stream) {
     size_t bytes = scratch_bytes;
-    return hipcub::DeviceRadixSort::SortPairsDescending(scratch, bytes, cost, cost_sorted, iota, order, n, 0,
-                                                        key_bits, stream);
+    return hipcub::DeviceRadixSort::SortPairsDescending(scratch, bytes, cost, cost_sorted, iota, order, n, 0, 9,
+                                                        stream);
 }
 
 #ifndef RT_PACKET_LEVELS

@@ -116,16 +116,6 @@ class Context:
     def set_stream(self, stream_handle: int):
         self._check(self.lib.rt_set_stream(self.h, C.c_void_p(stream_handle)))
 
-    def register_host_buffer(self, arr: np.ndarray):
-        """rt_register_host_buffer: page-lock and map a host output array;
-        rt_render into it then streams each finished row slab while the rest
-        of the frame renders.  Keep `arr` alive until unregistered."""
-        assert arr.flags.c_contiguous
-        self._check(self.lib.rt_register_host_buffer(self.h, C.c_void_p(arr.ctypes.data), C.c_size_t(arr.nbytes)))
-
-    def unregister_host_buffer(self, arr: np.ndarray):
-        self._check(self.lib.rt_unregister_host_buffer(self.h, C.c_void_p(arr.ctypes.data)))
-
     def set_scene(self, scene: Scene, build: int = abi.RT_BUILD_SAH_HOST):
         """Upload a scene and build its BVH: host SAH (4-wide) or on-device
         LBVH (2-wide, for per-frame rebuilds).  Renders are identical."""
