@@ -1,13 +1,10 @@
 """Device-math shortcuts must be bit-identical to the IEEE operations they
 replace (DESIGN.md "Arithmetic contract"):
 
-* rtm::rcp_cr — v_rcp_f32 + Newton step + Markstein correction for
-  2^-125 < |b| < 2^125 — against IEEE 1.0f / b, EVERY float in that range
-  (both signs, ~4.2e9 values, counted on the device);
 * rts::spec_pow_int — binary powering in double with a Ziv rounding test,
   falling back to the double pow — against the host's correctly rounded
   pow((double)x, (double)y) rounded to float (numpy float64 power).
-Both run through librt_selftest.so (test infrastructure, not the product ABI).
+It runs through librt_selftest.so (test infrastructure, not the product ABI).
 """
 import ctypes as C
 import os
@@ -24,18 +21,9 @@ LIB = os.path.join(ROOT, "unity-raytracer_amd", "lib", "librt_selftest.so")
 @pytest.fixture(scope="module")
 def st(rt):
     lib = C.CDLL(LIB)
-    lib.rt_selftest_rcp.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]
-    lib.rt_selftest_rcp.restype = C.c_longlong
     lib.rt_selftest_pow.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     lib.rt_selftest_pow.restype = C.c_int
     return lib
-
-
-def test_rcp_exhaustive(st):
-    first = C.c_uint32(0)
-    # bit patterns of 2^-125 (exclusive) .. 2^125 (exclusive), both signs
-    bad = st.rt_selftest_rcp(0x01000001, 0x7E000000, C.byref(first))
-    assert bad == 0, f"{bad} mismatches, first at bits {first.value:#010x}"
 
 
 def _pow_dev(st, x, y):

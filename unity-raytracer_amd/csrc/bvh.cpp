@@ -9,14 +9,8 @@
 namespace rtb {
 namespace {
 
-#ifndef RT_SAH_BINS
-#define RT_SAH_BINS 32
-#endif
-#ifndef RT_SAH_TRAVERSAL
-#define RT_SAH_TRAVERSAL 1.0f
-#endif
-constexpr int kBins = RT_SAH_BINS;
-constexpr float kTraversalCost = RT_SAH_TRAVERSAL;  // relative to one primitive test
+constexpr int kBins = 32;
+constexpr float kTraversalCost = 1.0f;  // relative to one primitive test
 constexpr float kIntersectCost = 1.0f;
 
 struct Box {

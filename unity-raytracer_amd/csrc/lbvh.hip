@@ -12,10 +12,7 @@ using rtm::f3;
 using rtm::mk;
 
 constexpr int kThreads = 256;
-#ifndef RT_LBVH_LEAF
-#define RT_LBVH_LEAF 4
-#endif
-constexpr int kLbvhLeaf = RT_LBVH_LEAF;  // max primitives per collapsed leaf (2-bit count field)
+constexpr int kLbvhLeaf = 4;  // max primitives per collapsed leaf (2-bit count field)
 
 inline int blocks_for(int n) { return (n + kThreads - 1) / kThreads; }
 

@@ -33,13 +33,6 @@ constexpr int kWaveStack = rtd::kStackTotal;  // 3 entries per BVH4 level
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
-#ifndef RT_PK_SIGNED
-#define RT_PK_SIGNED 1
-#endif
-#ifndef RT_PK_TOPCACHE
-#define RT_PK_TOPCACHE 1
-#endif
-
 // Wave-wide sort key of one child (bits of a float >= 0): +inf bits when no
 // lane needs it, the representative lane's entry distance when it hits,
 // FLT_MAX bits when only other lanes do.
@@ -138,7 +131,6 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
     int node = 0;  // wave-uniform
     int sp = 0;    // wave-uniform
     int wgate = -2;  // mesh whose gate every live lane has evaluated (gate_ok), wave-uniform
-#if RT_PK_TOPCACHE
     // the top entry of the wave stack is held in a register (all lanes the
     // same value); a pop hands it over at once and refills it from LDS, so
     // the LDS read overlaps the next node fetch instead of preceding it
@@ -149,10 +141,6 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
         topv = (v);                                 \
         ++sp;                                       \
     } while (0)
-#else
-#define RT_PK_PUSH(v) (wstack[sp++] = (v))
-#endif
-#if RT_PK_SIGNED
     // direction signs of the live lanes: uniform for most packets (camera
     // tiles, shadow rays of a tile towards one light)
     const unsigned long long live0 = __ballot(L.live);
@@ -161,14 +149,12 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
     const bool same_signs = (mx == 0 || mx == live0) && (my == 0 || my == live0) && (mz == 0 || mz == live0);
     // plane-row offsets in the node (lo, hi per axis): near row first
     const int ox = uni(same_signs && mx != 0), oy = uni(same_signs && my != 0), oz = uni(same_signs && mz != 0);
-#endif
     while (true) {
 #ifdef RT_SEG_PROFILE
         if (node >= 0) L.nodes++; else L.leaves++;
 #endif
         if (node >= 0) {
             float k0 = INFINITY, k1 = INFINITY, k2 = INFINITY, k3 = INFINITY;
-#if RT_PK_SIGNED
             const int4 ch = rtt::cload(&S.nodes4[node].child);
             if (same_signs) {
                 // the near and far plane rows of each axis are fetched
@@ -196,18 +182,6 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                     if (COUNT) cnt.box += 4;
                 }
             }
-#else
-            const rtd::BvhNode4 nd = rtt::cload(S.nodes4 + node);  // scalar loads
-            const int4 ch = nd.child;
-            if (L.live) {
-                const float4 lx = nd.lox, hx = nd.hix, ly = nd.loy, hy = nd.hiy, lz = nd.loz, hz = nd.hiz;
-                k0 = rtt::child_key(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, L.tcull);
-                k1 = rtt::child_key(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, L.tcull);
-                k2 = rtt::child_key(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, L.tcull);
-                k3 = rtt::child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, L.tcull);
-                if (COUNT) cnt.box += 4;
-            }
-#endif
             // wave-wide order: children nobody needs get +inf; the others are
             // ordered by the entry distance of a representative live lane
             // (children it misses go last).  Order only affects speed.  Keys
@@ -271,12 +245,8 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
         }
         if (sp == 0) return;
         --sp;
-#if RT_PK_TOPCACHE
         node = uni(topv);
         if (sp > 0) topv = wstack[sp - 1];
-#else
-        node = uni(wstack[sp]);
-#endif
     }
 #undef RT_PK_PUSH
 }

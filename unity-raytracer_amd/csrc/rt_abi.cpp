@@ -466,9 +466,6 @@ hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
     return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
 }
 
-#ifndef RT_SPLIT_DIV
-#define RT_SPLIT_DIV 256
-#endif
 // Quarter-wave splitting of a frame's slowest tiles trades extra work (each
 // quarter re-walks the BVH top) for a shorter critical path; it pays only
 // when the frame (shard) is small enough for its slowest wave to set its
@@ -477,28 +474,16 @@ hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
 // slowest of them (1/2048 of the tiles) go further, to sixteen waves of one
 // pixel each: a 1/8 shard's single frame -14 % more, throughput with frames
 // in flight +-1 % (1/512 or more: -5..-15 %).
-#ifndef RT_SPLIT16_DIV
-#define RT_SPLIT16_DIV 2048
-#endif
-constexpr int kSplit16Div = RT_SPLIT16_DIV;  // of those, 1/kSplit16Div of the tiles as sixteenth-waves; 0: off
-constexpr int kSplitDiv = RT_SPLIT_DIV;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
+constexpr int kSplit16Div = 2048;  // of those, 1/kSplit16Div of the tiles as sixteenth-waves; 0: off
+constexpr int kSplitDiv = 256;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
 // Larger shards (up to 70,000 tiles: a 1/2 or 1/4 shard of 1080p) split only
 // their slowest 1/4096 into sixteenth-waves: single frame -15..-30 %,
 // throughput with frames in flight +2..4 % on a 1/4 shard; a whole frame
 // (129,600 tiles) loses 2-6 % and does not split.
-#ifndef RT_SPLIT16_MAX_TILES
-#define RT_SPLIT16_MAX_TILES 70000
-#endif
-#ifndef RT_SPLIT16_DIV_LARGE
-#define RT_SPLIT16_DIV_LARGE 4096
-#endif
 constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this many tiles
-constexpr int kSplit16MaxTiles = RT_SPLIT16_MAX_TILES;
-constexpr int kSplit16DivLarge = RT_SPLIT16_DIV_LARGE;
-#ifndef RT_LPT_PERIOD
-#define RT_LPT_PERIOD 16
-#endif
-constexpr int kLptPeriod = RT_LPT_PERIOD;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
+constexpr int kSplit16MaxTiles = 70000;
+constexpr int kSplit16DivLarge = 4096;
+constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 // rt_render's host-output pipeline: about this many bytes per row slab, at most kMaxSlabs slabs
 constexpr size_t kSlabBytes = (size_t)6 << 20;
 constexpr int kMaxSlabs = 8;

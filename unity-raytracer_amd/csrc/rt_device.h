@@ -25,19 +25,10 @@
 
 namespace rtd {
 
-#ifndef RT_STACK_LDS
-#define RT_STACK_LDS 24
-#endif
-constexpr int kStackSize = RT_STACK_LDS;  // LDS traversal stack entries per lane
-#ifndef RT_STACK_TOTAL
-#define RT_STACK_TOTAL 128
-#endif
-constexpr int kStackTotal = RT_STACK_TOTAL;          // + private (scratch) overflow: >= 3 * BVH4 depth, >= LBVH depth
+constexpr int kStackSize = 24;  // LDS traversal stack entries per lane
+constexpr int kStackTotal = 128;         // + private (scratch) overflow: >= 3 * BVH4 depth, >= LBVH depth
 constexpr int kMaxTreeDepth = 31;         // builder guarantees BVH2 internal depth <= 31
-#ifndef RT_MAX_BOUNCES
-#define RT_MAX_BOUNCES 32
-#endif
-constexpr int kMaxBounces = RT_MAX_BOUNCES;     // per-lane mirror fold stack
+constexpr int kMaxBounces = 32;     // per-lane mirror fold stack
 constexpr int kWaveSize = 64;
 constexpr int kBlockThreads = 256;  // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;

@@ -37,13 +37,7 @@ RT_HD f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
 // fminf/fmaxf do; the two can differ only in which zero they return for
 // (-0, +0), and a slab test's outcome (tmin <= tmax) cannot tell the zeros
 // apart — so on the device the single-instruction v_min/v_max_f32 are used.
-#ifndef RT_SLAB_FMIN
-#define RT_SLAB_FMIN 1
-#endif
-#ifndef RT_RCP_FAST
-#define RT_RCP_FAST 0
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && RT_SLAB_FMIN
+#if defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ float slab_min(float x, float y) { return fminf(x, y); }
 __device__ __forceinline__ float slab_max(float x, float y) { return fmaxf(x, y); }
 #else
@@ -51,24 +45,9 @@ RT_HD float slab_min(float x, float y) { return (__builtin_isnan(y) || x < y) ? 
 RT_HD float slab_max(float x, float y) { return (__builtin_isnan(y) || x > y) ? x : y; }
 #endif
 
-// Correctly rounded 1.0f / b.  On the device, for 2^-125 < |b| < 2^125 (no
-// operand or result scaling needed) the hardware division sequence without
-// its scale/fixup steps: v_rcp_f32, one Newton step, one Markstein
-// correction (verified bit-exact against IEEE division for every float in
-// that range: tests/test_gpu_math.py); other b take the IEEE division.
-#if defined(__HIP_DEVICE_COMPILE__) && RT_RCP_FAST
-__device__ __forceinline__ float rcp_cr(float b) {
-    const float ab = fabsf(b);
-    if (__builtin_expect(!(ab > 0x1p-125f && ab < 0x1p125f), 0)) return 1.0f / b;
-    const float y = __builtin_amdgcn_rcpf(b);
-    const float e = fmaf(-b, y, 1.0f);
-    const float y1 = fmaf(e, y, y);
-    const float r = fmaf(-b, y1, 1.0f);
-    return fmaf(r, y1, y1);
-}
-#else
+// Correctly rounded 1.0f / b: the IEEE division (the kernels are compiled
+// with -fhip-fp32-correctly-rounded-divide-sqrt).
 RT_HD float rcp_cr(float b) { return 1.0f / b; }
-#endif
 
 RT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 RT_HD f3 cross(f3 x, f3 y) {

@@ -59,14 +59,7 @@ __device__ __forceinline__ ShadowRay shadow_ray(const Surface &s, const rtd::Dev
 // the double-precision polynomial constants are hoisted to the kernel entry
 // and spilled to scratch for the whole frame (64 B per lane written, then
 // reloaded serially in every light loop).
-#ifndef RT_POW_NOINLINE
-#define RT_POW_NOINLINE 1
-#endif
-#if RT_POW_NOINLINE
 __device__ __attribute__((noinline)) float spec_pow(float x, float y) { return (float)pow((double)x, (double)y); }
-#else
-__device__ __forceinline__ float spec_pow(float x, float y) { return (float)pow((double)x, (double)y); }
-#endif
 
 // (float)Math.Pow((double)x, (double)y) for the Phong exponents scenes use:
 // for an integer y in [1, 128], x^y by binary powering in double (relative
@@ -76,12 +69,9 @@ __device__ __forceinline__ float spec_pow(float x, float y) { return (float)pow(
 // then the result is the float nearest the exact power — which is what the
 // host's correctly rounded pow, rounded to float, also is.  Otherwise, and
 // for any other exponent, the out-of-line double pow.
-#ifndef RT_POW_INT
-#define RT_POW_INT 1
-#endif
 __device__ __forceinline__ float spec_pow_int(float x, float y) {
     const int n = (int)y;
-    if (RT_POW_INT && (float)n == y && n >= 1 && n <= 128) {
+    if ((float)n == y && n >= 1 && n <= 128) {
         double b = (double)x, r = (n & 1) ? b : 1.0;
         for (int e = n >> 1; e; e >>= 1) {
             b = b * b;

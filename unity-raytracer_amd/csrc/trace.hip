@@ -34,21 +34,10 @@ namespace {
 // Shade with the mirror recursion unrolled into a loop; the recursion's
 // results are folded back to front so c0 + km0*(c1 + km1*(...)) rounds
 // exactly like the reference.
-// RT_MK_PACKET_SHADOW: the first level's shadow rays (all from one pixel tile
-// towards the same light, highly coherent) are traced as one wave packet
-// (packet.h, scalar node fetches); deeper levels per lane.  All lanes in a
-// loop iteration are at the same depth, so the choice is wave-uniform.
-#ifndef RT_MK_PACKET_SHADOW
-#define RT_MK_PACKET_SHADOW 1
-#endif
-// RT_MK_PACKET_PRIMARY: the same for the camera rays (closest hit).
-#ifndef RT_MK_PACKET_PRIMARY
-#define RT_MK_PACKET_PRIMARY 1
-#endif
-// Depths (0 = camera rays) traced as packets.
-#ifndef RT_MK_PACKET_DEPTHS
-#define RT_MK_PACKET_DEPTHS 1
-#endif
+// The camera rays of a pixel tile and the first level's shadow rays (all
+// from one tile towards the same light, highly coherent) are traced as wave
+// packets (packet.h, scalar node fetches); deeper levels per lane.  All lanes
+// in a loop iteration are at the same depth, so the choice is wave-uniform.
 
 // RT_SEG_PROFILE (profiling builds only): per-wave shader-clock time of the
 // setup / camera-packet / first-level shadow-packet segments and the whole
@@ -260,16 +249,11 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     return col;
 }
 
-#ifndef RT_MK_MIN_WAVES
-#define RT_MK_MIN_WAVES 5
-#endif
+constexpr int kMkMinWaves = 5;  // waves per SIMD the register budget must allow (96 VGPRs)
 // Waves per megakernel workgroup.  A workgroup's slot is recycled only when
 // all of its waves are done, and path lengths vary a lot between tiles, so
 // small workgroups keep the CUs fuller near the end of each wave "round".
-#ifndef RT_MK_WAVES
-#define RT_MK_WAVES 1
-#endif
-constexpr int kMkWaves = RT_MK_WAVES;
+constexpr int kMkWaves = 1;
 constexpr int kMkThreads = kMkWaves * kWaveSize;
 
 
@@ -316,15 +300,14 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
 // the one for MaxReflectionBounces > kMaxBounces (deep_chain); Q4: frames of
 // 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel).
 template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false>
-__global__ __launch_bounds__(kMkThreads, RT_MK_MIN_WAVES) void render_kernel(SceneDev S, FrameDev F) {
+__global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
-    constexpr bool kPackets = RT_MK_PACKET_SHADOW || RT_MK_PACKET_PRIMARY;
-    __shared__ int wstack_mem[kPackets ? kMkWaves * rtp::kWaveStack : 1];
+    __shared__ int wstack_mem[kMkWaves * rtp::kWaveStack];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int ovf[kStackTotal - kStackSize];
     const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
-    int *const wstack = wstack_mem + (kPackets ? wave * rtp::kWaveStack : 0);
+    int *const wstack = wstack_mem + wave * rtp::kWaveStack;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x * kMkWaves + wave;
     const int split16 = SPLIT ? F.split16_tiles : 0;
@@ -536,23 +519,15 @@ __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int ba
 
 namespace rtk {
 
-#ifndef RT_MK_LEVELS
-#define RT_MK_LEVELS 1
-#endif
-#ifndef RT_MK_Q4
-#define RT_MK_Q4 1
-#endif
 // all-packet levels pay off where a wave's tile is small on screen (its
 // mirror rays stay coherent): 16+ samples per pixel = at most 2x2 pixels
-#ifndef RT_MK_LEVELS_MIN_SPP
-#define RT_MK_LEVELS_MIN_SPP 16
-#endif
+constexpr int kLevelsMinSpp = 16;
 
 
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
     const int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
-    const bool q4 = RT_MK_Q4 && F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
+    const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)
             hipLaunchKernelGGL((render_kernel<true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
@@ -564,7 +539,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
         hipLaunchKernelGGL((render_kernel<false, true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (F.split_tiles > 0 || F.split16_tiles > 0)
         hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    else if (RT_MK_LEVELS && S.bvh4 && F.spp >= RT_MK_LEVELS_MIN_SPP)
+    else if (S.bvh4 && F.spp >= kLevelsMinSpp)
         return launch_render_levels(S, F, stream);
     else if (q4)
         hipLaunchKernelGGL((render_kernel<false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
@@ -602,18 +577,15 @@ hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const
                                                         stream);
 }
 
-#ifndef RT_PACKET_LEVELS
-#define RT_PACKET_LEVELS 1
-#endif
 
 hipError_t launch_render_packet(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
     const int blocks = (F.num_tiles + kWavesPerBlock - 1) / kWavesPerBlock;
     if (count_tests)
-        hipLaunchKernelGGL((render_packet_kernel<true, RT_PACKET_LEVELS>), dim3(blocks), dim3(kBlockThreads), 0,
+        hipLaunchKernelGGL((render_packet_kernel<true, true>), dim3(blocks), dim3(kBlockThreads), 0,
                            stream, S, F);
     else
-        hipLaunchKernelGGL((render_packet_kernel<false, RT_PACKET_LEVELS>), dim3(blocks), dim3(kBlockThreads), 0,
+        hipLaunchKernelGGL((render_packet_kernel<false, true>), dim3(blocks), dim3(kBlockThreads), 0,
                            stream, S, F);
     return hipGetLastError();
 }

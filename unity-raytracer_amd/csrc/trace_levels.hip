@@ -22,9 +22,7 @@ using rtt::Counts;
 
 namespace {
 
-#ifndef RT_LV_MIN_WAVES
-#define RT_LV_MIN_WAVES 7
-#endif
+constexpr int kLvMinWaves = 7;
 
 // Level-synchronous all-packet megakernel (the default non-counting path on
 // a 4-wide BVH): one wave = one tile of 64 samples; the Whitted chain
@@ -35,7 +33,7 @@ namespace {
 // no spills); the mirror fold (c + km*(...), evaluated back to front as the
 // recursion rounds) lives in scratch and is touched only by mirror lanes.
 // Same arithmetic per sample as render_kernel.
-__global__ __launch_bounds__(kWaveSize, RT_LV_MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
+__global__ __launch_bounds__(kWaveSize, kLvMinWaves) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
     const int lane = threadIdx.x & 63;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
