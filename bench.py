@@ -580,8 +580,10 @@ def main():
     if rank == 0:
         avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's own trace kernel, HIP events
         pmc, pmc_state = load_pmc(args.config, lib_path)
-        kname = {"megakernel": "render_kernel<false, false, false>", "packet": "render_packet_kernel<false, 1>"}.get(
-            args.mode, "wavefront passes (sum)")
+        # the megakernel instance the frame ran: <COUNT, SPLIT, DEEP, Q4>, Q4 for 2x2 spp (4x4-pixel tiles)
+        q4 = "true" if fr.spp == 4 else "false"
+        kname = {"megakernel": f"render_kernel<false, false, false, {q4}>",
+                 "packet": "render_packet_kernel<false, true>"}.get(args.mode, "wavefront passes (sum)")
         rays_per_frame = rays // args.steps
         line = {
             "metric": METRIC,

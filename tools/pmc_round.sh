@@ -16,4 +16,4 @@ run B "TCC_EA0_WRREQ TCC_EA0_WRREQ_64B TCC_HIT TCC_MISS" &&
 run C "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" &&
 run D "SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_LEVEL_WAVES SQ_ACTIVE_INST_VMEM" &&
 python $R/tools/pmc_summary.py $R/gpurun_out/pmc_$tag/A $R/gpurun_out/pmc_$tag/B $R/gpurun_out/pmc_$tag/C $R/gpurun_out/pmc_$tag/D \
-  --kernel "render_kernel<false, false, false>" --out $R/gpurun_out/pmc_$tag/summary.json > /dev/null && echo pmc-ok
+  --kernel "render_kernel<false, false, false, true>" --out $R/gpurun_out/pmc_$tag/summary.json > /dev/null && echo pmc-ok
