@@ -163,6 +163,7 @@ struct rt_ctx {
     int4 *d_hits = nullptr;
     size_t rays_cap = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_slab0 = nullptr;  // rt_render's slab pipeline: the second stream starts after this point
     // RT_FLAG_ASYNC frames: pending count, accumulated counters and device time
     hipEvent_t ev_a0 = nullptr;
     int async_frames = 0;
@@ -192,6 +193,7 @@ struct rt_ctx {
     // rt_render's slab pipeline: copy stream + one event per slab
     hipStream_t copy_stream = nullptr;
     std::vector<hipEvent_t> slab_done;
+    hipStream_t slab_stream2 = nullptr;  // ... odd slabs render here, even ones on the context's stream
     // multi-device context: this context is member 0 (the root, device 0 of
     // the frame); peers[i] is member i + 1, a single-device context of its own
     std::vector<rt_ctx *> peers;
@@ -484,8 +486,9 @@ constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this
 constexpr int kSplit16MaxTiles = 70000;
 constexpr int kSplit16DivLarge = 4096;
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
-// rt_render's host-output pipeline: about this many bytes per row slab, at most kMaxSlabs slabs
-constexpr size_t kSlabBytes = (size_t)6 << 20;
+// rt_render's host-output pipeline: about this many bytes per row slab, at most kMaxSlabs slabs (C3:
+// 8 slabs of 4.1 MB in float RGBA, 4 of 2.1 MB in RGBA8), alternating over two streams
+constexpr size_t kSlabBytes = (size_t)2 << 20;
 constexpr int kMaxSlabs = 8;
 
 // Sums the sharded ray/test counters on the host (the stream must be idle).
@@ -705,8 +708,17 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         }
         const rtd::FrameDev F0 = F;
         std::vector<std::pair<LptSlot *, rtd::FrameDev>> sorts;
+        std::vector<hipStream_t> sort_streams;
         std::vector<std::pair<int, int>> bounds;
+        // slabs alternate between two streams, so a slab's tail overlaps the
+        // next slab instead of idling the GPU
+        const hipStream_t base = ctx->stream;
+        if (!ctx->slab_stream2) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->slab_stream2, hipStreamNonBlocking));
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_slab0, base));
+        HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->slab_stream2, ctx->ev_slab0, 0));
+        struct Restore { rt_ctx *c; hipStream_t s; ~Restore() { c->stream = s; } } restore{ctx, base};
         for (int k = 0; k < nslab; ++k) {
+            ctx->stream = (k & 1) ? ctx->slab_stream2 : base;
             const int r0 = std::min(F0.local_rows, (int)((long long)tile_rows * k / nslab) * F0.tile_h);
             const int r1 = std::min(F0.local_rows, (int)((long long)tile_rows * (k + 1) / nslab) * F0.tile_h);
             rtd::FrameDev Fk = F0;
@@ -721,14 +733,21 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             st = launch_frame(ctx, Fk, P, A, chunk_tiles);
             if (st) return st;
             HIP_OR_FAIL(ctx, hipEventRecord(ctx->slab_done[k], ctx->stream));
-            if (lpt_sort) sorts.emplace_back(ls, Fk);
+            if (lpt_sort) {
+                sorts.emplace_back(ls, Fk);
+                sort_streams.push_back(ctx->stream);
+            }
             bounds.emplace_back(r0, r1);
         }
-        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-        for (auto &so : sorts) {  // after the timed region: the order of the next frames
-            int st = lpt_sort_now(ctx, so.second, so.first);
+        ctx->stream = base;
+        if (nslab > 1) HIP_OR_FAIL(ctx, hipStreamWaitEvent(base, ctx->slab_done[nslab - (nslab & 1 ? 2 : 1)], 0));
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, base));
+        for (size_t i = 0; i < sorts.size(); ++i) {  // after the timed region: the order of the next frames
+            ctx->stream = sort_streams[i];
+            int st = lpt_sort_now(ctx, sorts[i].second, sorts[i].first);
             if (st) return st;
         }
+        ctx->stream = base;
         // every launch is enqueued before the first copy: a copy into pageable
         // memory may hold the host until it is done
         for (int k = 0; k < nslab; ++k) {
@@ -977,6 +996,7 @@ int create_one(int dev, rt_ctx **out) {
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->ev_a0) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_slab0, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_counters, rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long)) !=
             hipSuccess) {
         rt_destroy(c);
@@ -991,6 +1011,7 @@ void destroy_one(rt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+    if (ctx->slab_stream2) (void)hipStreamSynchronize(ctx->slab_stream2);
     free_scene(ctx);
     free_wavefront(ctx);
     ctx->lb.release();
@@ -1003,9 +1024,11 @@ void destroy_one(rt_ctx *ctx) {
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev_a0) (void)hipEventDestroy(ctx->ev_a0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->ev_slab0) (void)hipEventDestroy(ctx->ev_slab0);
     for (auto &se : ctx->async_end) (void)hipEventDestroy(se.second);
     for (hipEvent_t e : ctx->slab_done) (void)hipEventDestroy(e);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+    if (ctx->slab_stream2) (void)hipStreamDestroy(ctx->slab_stream2);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }
