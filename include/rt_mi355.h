@@ -319,8 +319,8 @@ int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t 
  * shard's rows are rendered and out_rgba receives the shard's compact
  * buffer (rt_band_rows_local rows); on a multi-device context such a frame
  * runs on device 0 only.  The device-to-host copy is overlapped with the
- * rendering: the frame is rendered in row slabs and each finished slab is
- * copied (through pinned staging) while the next ones render. */
+ * rendering: the frame is rendered in row slabs (alternating over two
+ * streams) and each finished slab is copied while later slabs render. */
 int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
               const rt_render_params *params, void *out_rgba, rt_stats *stats);
 
