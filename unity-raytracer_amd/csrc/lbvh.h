@@ -13,9 +13,11 @@
 //   4. Karras hierarchy: n-1 internal nodes in parallel;
 //   5. bottom-up padded boxes, second arrival continues (write-through sc1
 //      stores and sc1 loads: per-XCD L2s are not coherent on MI355X);
-//   6. node depths (climb to the root) -> even-depth flags -> scan;
-//   7. optional collapse to 4-wide nodes: every even-depth node adopts its
-//      grandchildren (leaf children keep their own slot).
+//   6. 2-wide depth (climb to the root; 2-wide output); small homogeneous subtrees marked
+//      as multi-primitive leaves; which 2-wide nodes stay as 4-wide nodes
+//      (walk from the root over the greedy slots below) -> scan;
+//   7. optional collapse to 4-wide nodes: each kept node expands, twice, its
+//      internal child slot of largest surface area (the host builder's rule).
 // Output: 2-wide nodes (rtd::BvhNode) and, when requested, 4-wide nodes
 // (rtd::BvhNode4), both with inline leaf refs and traversed by the same
 // kernels (SceneDev.bvh4).  Same padding rules as the host builder, so
@@ -63,8 +65,9 @@ struct LbvhOutput {
 // Scratch owned by the caller (grown with lbvh_scratch_bytes).
 size_t lbvh_scratch_bytes(int n);
 
-// Two device ints written by build_lbvh_gpu: the depth of the 2-wide tree
-// (levels, leaves included) and the 4-wide node count (when collapsed).
+// Three device ints written by build_lbvh_gpu: the depth of the 2-wide tree
+// (levels, leaves included; 2-wide output only), the 4-wide node count and
+// the depth of the deepest 4-wide node (root 0) (4-wide output only).
 const int *lbvh_info_ptr(const void *scratch, int n);
 
 // Builds on `stream`; returns the first HIP error.  n = mt + ns + nl >= 1.

@@ -292,18 +292,13 @@ __global__ void k_small(int n, const int2 *range, const int *gate_pos, int *smal
     small[i] = ok ? 1 : 0;
 }
 
-// 6b. depth of every internal node (climb to the root; depths are small);
-// 4-wide nodes are the even-depth nodes not inside a collapsed subtree.
-__global__ void k_depth(int n, const int *node_parent, const int *small, int *even, int *max_depth) {
+// 6b. depth of every internal node of the 2-wide tree (climb to the root;
+// depths are small): the traversal stack bound of the 2-wide layout.
+__global__ void k_depth(int n, const int *node_parent, int *max_depth) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n - 1) return;
     int d = 0;
-    bool inside = small[i] != 0;
-    for (int ps = node_parent[i]; ps >= 0; ps = node_parent[ps >> 1]) {
-        ++d;
-        inside = inside || small[ps >> 1] != 0;
-    }
-    even[i] = (d & 1) == 0 && !inside;
+    for (int ps = node_parent[i]; ps >= 0; ps = node_parent[ps >> 1]) ++d;
     // leaves sit one level below their parent
     atomicMax(max_depth, d + 1);
 }
@@ -316,16 +311,147 @@ __device__ __forceinline__ void read_slot(const rtd::BvhNode &nd, int side, floa
     }
 }
 
-// 7. collapse: an even-depth node adopts its grandchildren through internal
-// children (leaf children keep their slot); unused slots get +inf boxes and
-// the sentinel leaf.  Child node refs are renumbered by the exclusive scan of
-// the even flags (the root stays 0).
-__global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, const int *even, const int *idx4,
+// The (up to) four slots of the 4-wide node made from 2-wide node i: start
+// from its two children and expand, twice, the slot of largest surface area
+// among the internal children that are not collapsed leaves (first such slot
+// on ties) — the rule of the host builder's collapse (bvh.cpp collapse), so
+// the root-level slots of big subtrees are split first.  Deterministic, so
+// k_keep and k_collapse see the same slots.
+struct Slots4 {
+    int ref[4];    // 2-wide child refs: >= 0 internal node, < 0 leaf ref
+    int start[4];  // first leaf position of each slot (when ranges are given)
+    float lo[3][4], hi[3][4];
+    int k;
+};
+
+__device__ __forceinline__ float half_area(const float lo[3], const float hi[3]) {
+    const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+// A slot's first leaf: a left child starts where its parent does; a right
+// leaf child is its parent's last leaf (Karras: last == gamma + 1).
+__device__ __forceinline__ int slot_start(const int2 *range, int parent, int side, int ref) {
+    if (!range) return 0;
+    return side == 0 ? range[parent].x : ref >= 0 ? range[ref].x : range[parent].y;
+}
+
+__device__ __forceinline__ void expand4(const rtd::BvhNode *nodes, const int *small, const int2 *range,
+                                        bool any_internal, int i, Slots4 &S) {
+    const rtd::BvhNode nd = nodes[i];
+    S.ref[0] = nd.d.x;
+    S.ref[1] = nd.d.y;
+    S.k = 2;
+    for (int s = 0; s < 2; ++s) {
+        float l[3], h[3];
+        read_slot(nd, s, l, h);
+        for (int a = 0; a < 3; ++a) {
+            S.lo[a][s] = l[a];
+            S.hi[a][s] = h[a];
+        }
+        S.start[s] = slot_start(range, i, s, S.ref[s]);
+    }
+    while (any_internal && S.k < 4) {
+        int best = -1;
+        float best_a = -1.0f;
+        for (int s = 0; s < S.k; ++s) {
+            const int c = S.ref[s];
+            if (c < 0 || small[c]) continue;
+            const float l[3] = {S.lo[0][s], S.lo[1][s], S.lo[2][s]}, h[3] = {S.hi[0][s], S.hi[1][s], S.hi[2][s]};
+            const float ar = half_area(l, h);
+            if (ar > best_a) {
+                best_a = ar;
+                best = s;
+            }
+        }
+        if (best < 0) break;
+        const int p = S.ref[best];
+        const rtd::BvhNode cn = nodes[p];
+        const int gc[2] = {cn.d.x, cn.d.y}, dst[2] = {best, S.k};
+        for (int g = 0; g < 2; ++g) {
+            float l[3], h[3];
+            read_slot(cn, g, l, h);
+            for (int a = 0; a < 3; ++a) {
+                S.lo[a][dst[g]] = l[a];
+                S.hi[a][dst[g]] = h[a];
+            }
+            S.ref[dst[g]] = gc[g];
+            S.start[dst[g]] = slot_start(range, p, g, gc[g]);
+        }
+        ++S.k;
+    }
+}
+
+// 6c. every internal node's slots as if it were kept, sorted by first leaf
+// (unused: start INT_MAX) — 32 B per node, so the walk below makes one
+// round trip per step instead of re-expanding.
+__global__ void k_slots(int n, const rtd::BvhNode *nodes, const int *small, const int2 *range, int4 *rec) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n - 1 || small[x]) return;
+    Slots4 S;
+    expand4(nodes, small, range, true, x, S);
+    int r[4], st[4];
+    for (int k = 0; k < 4; ++k) {  // a collapsed-leaf child reads as a leaf (-1): the walk stops there
+        r[k] = k < S.k ? (S.ref[k] >= 0 && small[S.ref[k]] ? -1 : S.ref[k]) : -1;
+        st[k] = k < S.k ? S.start[k] : INT_MAX;
+    }
+    for (int a = 1; a < 4; ++a)  // insertion sort by start
+        for (int b = a; b > 0 && st[b - 1] > st[b]; --b) {
+            const int ts = st[b]; st[b] = st[b - 1]; st[b - 1] = ts;
+            const int tr = r[b]; r[b] = r[b - 1]; r[b - 1] = tr;
+        }
+    rec[2 * x] = make_int4(r[0], r[1], r[2], r[3]);
+    rec[2 * x + 1] = make_int4(st[0], st[1], st[2], st[3]);
+}
+
+// 6d. which 2-wide nodes become 4-wide nodes: the root, and every internal
+// slot (not a collapsed leaf) of a 4-wide node.  Each thread walks from the
+// root over 4-wide nodes towards its own node x (the slot whose leaf range
+// holds x's first leaf); x is kept when it is that slot, dropped when its
+// range spans several slots (it was expanded into the 4-wide node above it)
+// or lies inside a collapsed leaf.  Also the 4-wide depth (root 0), which
+// bounds the traversal stack.
+__global__ void k_keep(int n, const int4 *rec, const int *small, const int2 *range, int *keep, int *depth4) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= n - 1) return;
+    if (x == 0) {
+        keep[0] = 1;
+        return;
+    }
+    const int2 rx = range[x];
+    int kept = 0, K = 0, kend = n - 1, lvl = 0;
+    if (!small[x]) {
+        while (true) {
+            const int4 rr = rec[2 * K], ss = rec[2 * K + 1];
+            const int r[4] = {rr.x, rr.y, rr.z, rr.w}, st[4] = {ss.x, ss.y, ss.z, ss.w};
+            int s = 0;
+            for (int k = 1; k < 4; ++k)
+                if (st[k] <= rx.x) s = k;
+            const int end = s < 3 && st[s + 1] != INT_MAX ? st[s + 1] - 1 : kend;
+            const int c = r[s];
+            if (c < 0 || rx.y > end) break;  // inside a (collapsed) leaf, or expanded into K's node
+            ++lvl;
+            if (c == x) {
+                kept = 1;
+                break;
+            }
+            K = c;
+            kend = end;
+        }
+    }
+    keep[x] = kept;
+    if (kept) atomicMax(depth4, lvl);
+}
+
+// 7. collapse: every kept node writes its 4-wide node from its expanded
+// slots; unused slots get +inf boxes and the sentinel leaf.  Child node refs
+// are renumbered by the exclusive scan of the keep flags (the root stays 0).
+__global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, const int *keep, const int *idx4,
                            const int *small, const int2 *range, const int *sph_idx, const int *is_sph,
                            rtd::BvhNode4 *out, int *info) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) info[1] = n > 1 ? idx4[n - 2] + even[n - 2] : 1;  // 4-wide node count
-    if (i >= (n > 1 ? n - 1 : 1) || (n > 1 && !even[i])) return;
+    if (i == 0) info[1] = n > 1 ? idx4[n - 2] + keep[n - 2] : 1;  // 4-wide node count
+    if (i >= (n > 1 ? n - 1 : 1) || (n > 1 && !keep[i])) return;
     // ref of an internal node c seen from a 4-wide node: a multi-primitive
     // leaf when its subtree is small, else its 4-wide index
     auto sub = [&](int c) {
@@ -336,56 +462,32 @@ __global__ void k_collapse(int n, int empty_ref, const rtd::BvhNode *nodes, cons
         return rtd::encode_leaf(sph ? sph_idx[f] : f - sph_idx[f], r.y - r.x + 1,
                                 sph ? rtd::kLeafSphere : rtd::kLeafTri);
     };
-    float lo[3][4], hi[3][4];
-    int ref[4];
-    int k = 0;
-    const rtd::BvhNode nd = nodes[i];
-    const int ch[2] = {nd.d.x, nd.d.y};
-    for (int s = 0; s < 2; ++s) {
-        if (ch[s] >= 0 && n > 1 && !small[ch[s]]) {
-            const rtd::BvhNode cn = nodes[ch[s]];
-            const int gc[2] = {cn.d.x, cn.d.y};
-            for (int g = 0; g < 2; ++g) {
-                float l[3], h[3];
-                read_slot(cn, g, l, h);
-                for (int a = 0; a < 3; ++a) {
-                    lo[a][k] = l[a];
-                    hi[a][k] = h[a];
-                }
-                ref[k++] = gc[g] >= 0 ? sub(gc[g]) : gc[g];
-            }
-        } else {
-            float l[3], h[3];
-            read_slot(nd, s, l, h);
-            for (int a = 0; a < 3; ++a) {
-                lo[a][k] = l[a];
-                hi[a][k] = h[a];
-            }
-            ref[k++] = (ch[s] >= 0 && n > 1) ? sub(ch[s]) : ch[s];
-        }
-    }
-    for (; k < 4; ++k) {
+    Slots4 S;
+    expand4(nodes, small, nullptr, n > 1, i, S);
+    for (int k = 0; k < S.k; ++k)
+        if (S.ref[k] >= 0 && n > 1) S.ref[k] = sub(S.ref[k]);
+    for (int k = S.k; k < 4; ++k) {
         for (int a = 0; a < 3; ++a) {
-            lo[a][k] = INFINITY;
-            hi[a][k] = INFINITY;
+            S.lo[a][k] = INFINITY;
+            S.hi[a][k] = INFINITY;
         }
-        ref[k] = empty_ref;
+        S.ref[k] = empty_ref;
     }
     rtd::BvhNode4 o;
-    o.lox = make_float4(lo[0][0], lo[0][1], lo[0][2], lo[0][3]);
-    o.hix = make_float4(hi[0][0], hi[0][1], hi[0][2], hi[0][3]);
-    o.loy = make_float4(lo[1][0], lo[1][1], lo[1][2], lo[1][3]);
-    o.hiy = make_float4(hi[1][0], hi[1][1], hi[1][2], hi[1][3]);
-    o.loz = make_float4(lo[2][0], lo[2][1], lo[2][2], lo[2][3]);
-    o.hiz = make_float4(hi[2][0], hi[2][1], hi[2][2], hi[2][3]);
-    o.child = make_int4(ref[0], ref[1], ref[2], ref[3]);
+    o.lox = make_float4(S.lo[0][0], S.lo[0][1], S.lo[0][2], S.lo[0][3]);
+    o.hix = make_float4(S.hi[0][0], S.hi[0][1], S.hi[0][2], S.hi[0][3]);
+    o.loy = make_float4(S.lo[1][0], S.lo[1][1], S.lo[1][2], S.lo[1][3]);
+    o.hiy = make_float4(S.hi[1][0], S.hi[1][1], S.hi[1][2], S.hi[1][3]);
+    o.loz = make_float4(S.lo[2][0], S.lo[2][1], S.lo[2][2], S.lo[2][3]);
+    o.hiz = make_float4(S.hi[2][0], S.hi[2][1], S.hi[2][2], S.hi[2][3]);
+    o.child = make_int4(S.ref[0], S.ref[1], S.ref[2], S.ref[3]);
     o.pad = make_int4(0, 0, 0, 0);
     out[n > 1 ? idx4[i] : 0] = o;
 }
 
 struct Layout {
     size_t keys_a, keys_b, vals_a, vals_b, plo, phi, tri_rank, is_sph, sph_idx, slo, shi, leaf_ref, leaf_parent,
-        node_parent, flags, even, idx4, depth, range, gate_pos, small, cub, total;
+        node_parent, flags, keep, idx4, rec, depth, range, gate_pos, small, cub, total;
     size_t cub_bytes;
 };
 
@@ -414,9 +516,10 @@ Layout layout(int n) {
     L.leaf_parent = take(sizeof(int) * n);
     L.node_parent = take(sizeof(int) * n);
     L.flags = take(sizeof(int) * n);
-    L.even = take(sizeof(int) * n);
+    L.keep = take(sizeof(int) * n);
     L.idx4 = take(sizeof(int) * n);
-    L.depth = take(2 * sizeof(int));  // depth, 4-wide node count
+    L.rec = take(2 * sizeof(int4) * n);
+    L.depth = take(3 * sizeof(int));  // 2-wide depth, 4-wide node count, 4-wide depth
     L.range = take(sizeof(int2) * n);
     L.gate_pos = take(sizeof(int) * n);
     L.small = take(sizeof(int) * n);
@@ -477,23 +580,24 @@ hipError_t build_lbvh_gpu(const LbvhInput &in, const LbvhOutput &out, void *scra
     hipLaunchKernelGGL(k_bounds, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, slo, shi, leaf_parent,
                        node_parent, out.nodes, flags);
     int *depth = (int *)(b + L.depth);
-    e = hipMemsetAsync(depth, 0, 2 * sizeof(int), stream);
+    e = hipMemsetAsync(depth, 0, 3 * sizeof(int), stream);
     if (e != hipSuccess) return e;
     if (n > 1) {
-        int *even = (int *)(b + L.even), *idx4 = (int *)(b + L.idx4);
-        hipLaunchKernelGGL(k_small, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, range, gate_pos, small);
-        if (!out.nodes4) {  // 2-wide output: no collapsed leaves
-            e = hipMemsetAsync(small, 0, sizeof(int) * n, stream);
-            if (e != hipSuccess) return e;
-        }
-        hipLaunchKernelGGL(k_depth, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, node_parent, small, even,
-                           depth);
-        if (out.nodes4) {
+        int *keep = (int *)(b + L.keep), *idx4 = (int *)(b + L.idx4);
+        if (!out.nodes4)  // the 2-wide stack bound; the 4-wide one comes from k_keep
+            hipLaunchKernelGGL(k_depth, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, node_parent, depth);
+        else {
+            hipLaunchKernelGGL(k_small, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, range, gate_pos, small);
+            int4 *rec = (int4 *)(b + L.rec);
+            hipLaunchKernelGGL(k_slots, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, out.nodes, small, range,
+                               rec);
+            hipLaunchKernelGGL(k_keep, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, rec, small, range, keep,
+                               depth + 2);
             cub_bytes = L.cub_bytes;
-            e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, even, idx4, n - 1, stream);
+            e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, keep, idx4, n - 1, stream);
             if (e != hipSuccess) return e;
             hipLaunchKernelGGL(k_collapse, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n,
-                               rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, even, idx4, small, range,
+                               rtd::encode_leaf(in.mt + in.nl, 1, rtd::kLeafTri), out.nodes, keep, idx4, small, range,
                                sph_idx, is_sph, out.nodes4, depth);
         }
     } else if (out.nodes4) {

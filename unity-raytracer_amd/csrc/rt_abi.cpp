@@ -858,11 +858,11 @@ int run_lbvh(rt_ctx *ctx, const rtl::LbvhInput &in, bool wide, rtd::SceneDev &S,
     float ms = 0.0f;
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->info.build_ms += ms;
-    int binfo[2] = {0, 0};
+    int binfo[3] = {0, 0, 0};  // 2-wide depth, 4-wide node count, 4-wide depth
     HIP_OR_FAIL(ctx, hipMemcpy(binfo, rtl::lbvh_info_ptr(B.scratch.p, P), sizeof(binfo), hipMemcpyDeviceToHost));
-    ctx->last_bvh_depth = binfo[0];
+    ctx->last_bvh_depth = wide ? binfo[2] : binfo[0];
     // traversal stack: one entry per 2-wide level, three per 4-wide level
-    const int need = wide ? 3 * ((binfo[0] + 1) / 2 + 1) : binfo[0] + 1;
+    const int need = wide ? 3 * (binfo[2] + 1) : binfo[0] + 1;
     if (need > rtd::kStackTotal)
         return fail(ctx, RT_E_SCENE, "LBVH depth %d exceeds the traversal stack; use RT_BUILD_SAH_HOST", binfo[0]);
     S.nodes = (const rtd::BvhNode *)B.nodes.p;
