@@ -489,6 +489,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     rays = st.primary_rays + st.shadow_rays + st.reflection_rays
+    moot = int(st.shadow_rays_moot)  # counted in rays, answered without a traversal
     # kernel-only device time of this rank's trace launch: the same frames
     # back to back without the gather, HIP events on the context's stream
     for _ in range(args.steps):
@@ -565,7 +566,7 @@ def main():
                 print(json.dumps(diag), file=sys.stderr, flush=True)
                 raise SystemExit("sharded frame differs from the single-rank frame")
     if dist_on:
-        t = torch.tensor([elapsed, float(rays), kernel_ms, float(scene_misses)], dtype=torch.float64,
+        t = torch.tensor([elapsed, float(rays), kernel_ms, float(scene_misses), float(moot)], dtype=torch.float64,
                          device="cpu" if gloo else "cuda")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -574,6 +575,7 @@ def main():
         rays = int(t[1])
         kernel_ms_max = float(tmax[2])
         scene_misses = int(t[3])
+        moot = int(t[4])
     else:
         kernel_ms_max = kernel_ms
 
@@ -613,6 +615,10 @@ def main():
                 "rays_trivial_miss": scene_misses,
                 "rays_in_scene": rays_per_frame - scene_misses,
                 "mrays_per_s_in_scene": (rays_per_frame - scene_misses) * args.steps / elapsed / 1e6,
+                # shadow rays whose answer cannot change the pixel (a light
+                # behind the surface): counted above, not traversed
+                "shadow_rays_moot": moot // args.steps,
+                "mrays_per_s_traversed": (rays - moot) / elapsed / 1e6,
                 "frames_in_flight": nstreams,
                 "frames_per_gather": G if dist_on else None,
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,

@@ -102,6 +102,7 @@ namespace RayTracer.Native
         public ulong PrimaryRays, ShadowRays, ReflectionRays, BoxTests, TriangleTests, SphereTests, ShadingFetches;
         public double KernelMs, TotalMs;
         public ulong PrimarySceneMisses;
+        public ulong ShadowRaysMoot;  // shadow rays whose answer cannot change the pixel (not traversed)
     }
 
     // rt_device_info: the GPUs one context drives (rt_create(N > 1)).

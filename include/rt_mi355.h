@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum rt_status {
@@ -181,6 +181,11 @@ typedef struct rt_stats {
     uint64_t primary_scene_misses; /* camera samples rejected by the Scene.AABB gate
                                       (Scene.cs:54) before any object test
                                       (RT_FLAG_COUNT_TESTS)                         */
+    uint64_t shadow_rays_moot; /* shadow rays (counted in shadow_rays) whose answer
+                                  cannot change the pixel — the light's unoccluded
+                                  term leaves the colour's bits unchanged, e.g. a
+                                  light behind the surface — so they were not
+                                  traversed (0 in RT_FLAG_COUNT_TESTS frames)      */
 } rt_stats;
 
 /* Closest-hit record, IntersectionResult (Data/Collision/IntersectionResult.cs:3-7)

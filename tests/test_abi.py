@@ -46,7 +46,7 @@ def test_ctypes_layouts(rt):
     sizes = {
         a.rt_float3: 12, a.rt_triangle: 36, a.rt_sphere: 16, a.rt_aabb: 24, a.rt_material: 56,
         a.rt_point_light: 24, a.rt_camera: 48, a.rt_scene_info: 32, a.rt_mesh_source: 152, a.rt_image_plane: 20, a.rt_mesh: 88, a.rt_hit: 16,
-        a.rt_ray: 24, a.rt_render_params: 40, a.rt_stats: 80, a.rt_device_info: 72,
+        a.rt_ray: 24, a.rt_render_params: 40, a.rt_stats: 88, a.rt_device_info: 72,
     }
     for t, s in sizes.items():
         assert C.sizeof(t) == s, t.__name__
@@ -60,11 +60,11 @@ def test_c_layouts_match(tmp_path):
 #include <stddef.h>
 #include "rt_mi355.h"
 int main(void){
- printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_mesh),
+ printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rt_material), sizeof(rt_mesh),
    sizeof(rt_scene_desc), sizeof(rt_render_params), sizeof(rt_stats), offsetof(rt_scene_desc, ambient_radiance),
    offsetof(rt_mesh, aabb), offsetof(rt_stats, kernel_ms), sizeof(rt_mesh_source),
    offsetof(rt_mesh_source, local_to_world), offsetof(rt_mesh_source, material), sizeof(rt_scene_info),
-   offsetof(rt_stats, primary_scene_misses), sizeof(rt_device_info));
+   offsetof(rt_stats, primary_scene_misses), sizeof(rt_device_info), offsetof(rt_stats, shadow_rays_moot));
  return 0; }''')
     exe = tmp_path / "l"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(prog)], check=True)
@@ -75,7 +75,7 @@ int main(void){
             C.sizeof(a.rt_stats), a.rt_scene_desc.ambient_radiance.offset, a.rt_mesh.aabb.offset,
             a.rt_stats.kernel_ms.offset, C.sizeof(a.rt_mesh_source), a.rt_mesh_source.local_to_world.offset,
             a.rt_mesh_source.material.offset, C.sizeof(a.rt_scene_info), a.rt_stats.primary_scene_misses.offset,
-            C.sizeof(a.rt_device_info)]
+            C.sizeof(a.rt_device_info), a.rt_stats.shadow_rays_moot.offset]
     assert vals == want
 
 

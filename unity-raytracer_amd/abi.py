@@ -13,7 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "librt_mi355.so")
 
-RT_ABI_VERSION = 2
+RT_ABI_VERSION = 3
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -147,6 +147,7 @@ class rt_stats(C.Structure):
         ("kernel_ms", C.c_double),
         ("total_ms", C.c_double),
         ("primary_scene_misses", C.c_uint64),
+        ("shadow_rays_moot", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -512,6 +512,7 @@ void fill_stats(rt_stats *stats, const unsigned long long counts[rtd::kCounterWo
     stats->sphere_tests = counts[5];
     stats->shading_fetches = counts[6];
     stats->primary_scene_misses = counts[7];
+    stats->shadow_rays_moot = counts[8];
     stats->kernel_ms = kernel_ms;
     stats->total_ms = total_ms;
 }

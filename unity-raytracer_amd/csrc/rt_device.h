@@ -37,7 +37,7 @@ constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;
 // 64-B line) per slot; the host sums the slots.  One shared word would
 // serialise every wave's atomics (a single word saturates near 88 atomics/us).
 constexpr int kCounterSlots = 256;
-constexpr int kCounterWords = 8;
+constexpr int kCounterWords = 16;  // one 128-B slot: words 0-8 used (rt_stats order)
 
 constexpr int kLeafTri = 0;
 constexpr int kLeafSphere = 1;
@@ -177,7 +177,7 @@ struct FrameDev {
     int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F / kOutRGB32F
     int split16_tiles;       // render_kernel: the first split16_tiles of tile_order run as 16 sixteenth-waves each,
     int split_tiles;         // ... the next split_tiles as 4 quarter-waves each
-    unsigned long long *counters;  // kCounterSlots x 8 u64, rt_stats order
+    unsigned long long *counters;  // kCounterSlots x kCounterWords u64, rt_stats order
 };
 
 }  // namespace rtd

@@ -106,6 +106,16 @@ __device__ __forceinline__ f3 light_term(const rtd::SceneDev &S, const Surface &
     return diffuse + spec;
 }
 
+// A light whose unoccluded term leaves the running colour's bits unchanged
+// (a light behind the surface: diffuse and specular are +0) yields the same
+// colour whether its shadow ray (:332-343) is blocked or not, so the ray's
+// answer is moot and it need not be traced.  Bitwise, so exact for every
+// input (signed zeros, NaN, overflow included).
+__device__ __forceinline__ bool same_bits(f3 a, f3 b) {
+    return __float_as_uint(a.x) == __float_as_uint(b.x) && __float_as_uint(a.y) == __float_as_uint(b.y) &&
+           __float_as_uint(a.z) == __float_as_uint(b.z);
+}
+
 // Reflect :368-373 (direction not re-normalised)
 __device__ __forceinline__ void reflect(const Surface &s, f3 &o, f3 &d) {
     o = s.p + s.n * rtm::kShadowEpsilon;

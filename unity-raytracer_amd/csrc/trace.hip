@@ -228,15 +228,19 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
         const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
         cnt.shadow++;
+        // a moot shadow ray (shade.h same_bits) is not traced
+        const f3 lit = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+        const bool moot = rts::same_bits(lit, col);
+        cnt.moot += moot;
         rtt::RayCtx rs;
         rtt::setup_ray(rs, sr.o, sr.dir);
         rtp::PacketLane Q;
         RT_SEG(const unsigned long long tw0 = __builtin_amdgcn_s_memtime();)
-        rtp::packet_trace<true, COUNT>(S, rs, true, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
+        rtp::packet_trace<true, COUNT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
         RT_SEG(sg.shadow += __builtin_amdgcn_s_memtime() - tw0;
                sg.visits += Q.nodes + ((unsigned long long)Q.leaves << 32);)
-        if (Q.best_rank == 1) continue;
-        col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+        if (moot || Q.best_rank == 1) continue;
+        col = lit;
     }
     const DevMaterial m = S.mats[sf.mat];
     if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363

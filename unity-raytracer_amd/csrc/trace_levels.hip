@@ -77,11 +77,15 @@ __global__ __launch_bounds__(kWaveSize, kLvMinWaves) void render_levels_kernel(S
             const DevLight Lt = S.lights[l];
             const rts::ShadowRay sr = rts::shadow_ray(sf, Lt);
             if (hit) cnt.shadow++;
+            // a moot shadow ray (shade.h same_bits) is not traced
+            const f3 lit = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
+            const bool trace = hit && !rts::same_bits(lit, col);
+            cnt.moot += hit && !trace;
             rtt::RayCtx rs;
             rtt::setup_ray(rs, sr.o, sr.dir);
             rtp::PacketLane Q;
-            rtp::packet_trace<true, false>(S, rs, hit, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
-            if (hit && Q.best_rank != 1) col = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
+            rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+            if (trace && Q.best_rank != 1) col = lit;
         }
         bool mirror = false;
         if (hit) {

@@ -23,6 +23,7 @@ using rtm::mk;
 struct Counts {
     unsigned primary, shadow, reflection, box, tri, sph, shading;
     unsigned scene_miss;  // camera samples rejected by the scene AABB gate (Scene.cs:54), COUNT launches
+    unsigned moot;        // shadow rays whose answer cannot change the colour: not traced (shade.h same_bits)
 };
 
 __device__ __forceinline__ float nudge(float v) { return fabsf(v) > 1e-20f ? v : copysignf(1e-20f, v); }
@@ -402,7 +403,8 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 template <bool COUNT>
 __device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long *counters) {
     unsigned long long *ctr = counters + (size_t)(blockIdx.x % rtd::kCounterSlots) * rtd::kCounterWords;
-    const unsigned p = wave_sum(c.primary), s = wave_sum(c.shadow), r = wave_sum(c.reflection);
+    const unsigned p = wave_sum(c.primary), s = wave_sum(c.shadow), r = wave_sum(c.reflection),
+                   m = wave_sum(c.moot);
     unsigned b = 0, t = 0, q = 0, h = 0, g = 0;
     if (COUNT) {
         b = wave_sum(c.box);
@@ -415,6 +417,7 @@ __device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long
         if (p) atomicAdd(ctr + 0, (unsigned long long)p);
         if (s) atomicAdd(ctr + 1, (unsigned long long)s);
         if (r) atomicAdd(ctr + 2, (unsigned long long)r);
+        if (m) atomicAdd(ctr + 8, (unsigned long long)m);
         if (COUNT) {
             if (b) atomicAdd(ctr + 3, (unsigned long long)b);
             if (t) atomicAdd(ctr + 4, (unsigned long long)t);
