@@ -91,6 +91,23 @@ def test_modes_bit_identical_full_c3(gpu_ctx, rt):
                                                                          sb.reflection_rays), flags
 
 
+@pytest.mark.parametrize("name,res,spp", [("C3", (96, 54), 4), ("C2", (96, 54), 4), ("C5", (48, 27), 16)])
+def test_moot_shadow_rays_are_invisible(gpu_ctx, rt, orc, name, res, spp):
+    """Shadow rays whose answer cannot change the pixel (shade.h same_bits:
+    the light's unoccluded term leaves the colour's bits unchanged) are not
+    traversed by the packet paths: they are still counted in shadow_rays (the
+    oracle's count), reported in shadow_rays_moot, and the frame equals the
+    oracle's and the counting launch's, which traces every ray per lane."""
+    fr = rt.make(name).with_resolution(*res).with_(spp=spp)
+    img, st = _render(gpu_ctx, rt, fr)
+    ref, counts = orc.render(fr)
+    _check(img, ref, st, counts, name)
+    assert 0 < st.shadow_rays_moot < st.shadow_rays
+    cimg, cst = _render(gpu_ctx, rt, fr, flags=1)
+    assert cst.shadow_rays_moot == 0
+    assert np.array_equal(img.view(np.uint32), cimg.view(np.uint32))
+
+
 def test_goldens(gpu_ctx, rt):
     """Committed fixtures (tests/golden/, made by tests/golden/make_golden.py)."""
     import os
