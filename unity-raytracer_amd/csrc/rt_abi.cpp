@@ -45,11 +45,11 @@ struct LbvhBufs {
     GrowBuf meshes, mesh_tris, mesh_normals, spheres, sphere_mat, loose_tris, loose_normals, loose_mat;
     GrowBuf nodes, nodes4, tris, sphs, shade, scratch;
     // device mesh extraction (scene_xform.hip): resident sources + matrices
-    GrowBuf src_meshes, src_local, src_indices, src_matrices, src_world, src_aabbs;
+    GrowBuf src_meshes, src_local, src_indices, src_matrices, src_world, src_aabbs, src_parts;
     void release() {
         GrowBuf *all[] = {&meshes, &mesh_tris, &mesh_normals, &spheres, &sphere_mat, &loose_tris, &loose_normals,
                           &loose_mat, &nodes, &nodes4, &tris, &sphs, &shade, &scratch, &src_meshes, &src_local,
-                          &src_indices, &src_matrices, &src_world, &src_aabbs};
+                          &src_indices, &src_matrices, &src_world, &src_aabbs, &src_parts};
         for (GrowBuf *b : all) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
@@ -82,7 +82,7 @@ constexpr int kLptSlots = 16;  // streams x row slabs
 // State kept by rt_set_scene_source for rt_update_mesh_transforms.
 struct SourceState {
     bool active = false;
-    int mesh_count = 0, vertex_total = 0, tri_total = 0;
+    int mesh_count = 0, vertex_total = 0, tri_total = 0, part_total = 0;
     float rest_lo[3], rest_hi[3];  // Scene.CalculateAABB over loose triangles and spheres
     rtl::LbvhInput in{};           // device inputs of the last build
     bool wide = true;
@@ -957,6 +957,8 @@ int extract_meshes(rt_ctx *ctx, std::vector<rtd::MeshGate> &aabbs, float &ms) {
     a.tris = (float *)B.mesh_tris.p;
     a.normals = (float *)B.mesh_normals.p;
     a.aabbs = (rtd::MeshGate *)B.src_aabbs.p;
+    a.part_total = ctx->src.part_total;
+    a.parts = (rtd::MeshGate *)B.src_parts.p;
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     HIP_OR_FAIL(ctx, rtx::transform_meshes(a, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
@@ -1676,11 +1678,13 @@ int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_s
     std::vector<rtx::MeshSrcDev> md((size_t)mesh_count);
     std::vector<float> local((size_t)vt * 3), mats((size_t)mesh_count * 16);
     std::vector<int> idx((size_t)tt * 3);
+    int parts = 0;  // AABB-reduction parts (scene_xform.hip k_aabb_parts)
     {
         int v = 0, t = 0;
         for (int m = 0; m < mesh_count; ++m) {
             const rt_mesh_source &M = meshes[m];
-            md[m] = {v, M.vertex_count, t, M.index_count / 3};
+            md[m] = {v, M.vertex_count, t, M.index_count / 3, parts};
+            parts += std::max(1, (M.vertex_count + rtx::kAabbPart - 1) / rtx::kAabbPart);
             if (M.vertex_count) std::memcpy(&local[(size_t)v * 3], M.vertices, sizeof(rt_float3) * M.vertex_count);
             std::memcpy(&mats[(size_t)m * 16], M.local_to_world, sizeof(float) * 16);
             for (int i = 0; i < M.index_count; ++i) {
@@ -1702,11 +1706,13 @@ int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_s
     HIP_OR_FAIL(ctx, put(ctx, B.src_matrices, mats.data(), mats.size()));
     HIP_OR_FAIL(ctx, ensure(ctx, B.src_world, sizeof(float) * 3 * (size_t)vt));
     HIP_OR_FAIL(ctx, ensure(ctx, B.src_aabbs, sizeof(rtd::MeshGate) * (size_t)mesh_count));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.src_parts, sizeof(rtd::MeshGate) * (size_t)std::max(parts, 1)));
     HIP_OR_FAIL(ctx, ensure(ctx, B.mesh_tris, sizeof(rt_triangle) * (size_t)tt));
     HIP_OR_FAIL(ctx, ensure(ctx, B.mesh_normals, sizeof(rt_float3) * (size_t)tt));
     ctx->src.mesh_count = mesh_count;
     ctx->src.vertex_total = (int)vt;
     ctx->src.tri_total = (int)tt;
+    ctx->src.part_total = parts;
     std::vector<rtd::MeshGate> aabbs;
     float xform_ms = 0.0f;
     int st = extract_meshes(ctx, aabbs, xform_ms);

@@ -24,7 +24,10 @@ struct MeshSrcDev {
     int vertex_count;
     int tri_first;     // geometry index of the mesh's first triangle
     int tri_count;
+    int part_first;    // first of the mesh's AABB parts (max(1, ceil(vertex_count / kAabbPart)) each)
 };
+
+constexpr int kAabbPart = 2048;  // vertices per AABB-reduction wave
 
 struct XformArgs {
     int mesh_count, vertex_total, tri_total;
@@ -36,6 +39,8 @@ struct XformArgs {
     float *tris;               // tri_total x 9 (rt_triangle layout)
     float *normals;            // tri_total x 3
     rtd::MeshGate *aabbs;      // mesh_count: exact Mesh.AABB
+    int part_total;            // AABB parts over all meshes
+    rtd::MeshGate *parts;      // part_total (scratch): per-part partial AABBs
 };
 
 hipError_t transform_meshes(const XformArgs &a, hipStream_t stream);

@@ -51,16 +51,24 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // Mesh.AABB: Min = float.MaxValue, Max = float.MinValue (= -FLT_MAX), then
 // Encapsulate(point) = min(point, Min) / max(point, Max) for every vertex
-// (AABB.cs:10-14).  One wave per mesh; a NaN coordinate never enters
-// (Unity's min(x, y) keeps y unless y is NaN or x < y), so the partial
-// results are NaN-free and their combination order does not matter.
-__global__ void k_aabbs(XformArgs a) {
-    const int m = (blockIdx.x * blockDim.x + threadIdx.x) / rtd::kWaveSize;
+// (AABB.cs:10-14).  A NaN coordinate never enters (Unity's min(x, y) keeps y
+// unless y is NaN or x < y), so partial results are NaN-free and their
+// combination order does not matter.  Two passes, so one big mesh does not
+// fall to a single wave (C3's knot: 35k vertices, 158 us): one wave per part
+// of kAabbPart vertices of a mesh, then one thread per mesh over its parts.
+__global__ void k_aabb_parts(XformArgs a) {
+    const int w = (blockIdx.x * blockDim.x + threadIdx.x) / rtd::kWaveSize;
     const int lane = threadIdx.x % rtd::kWaveSize;
-    if (m >= a.mesh_count) return;
-    const MeshSrcDev M = a.meshes[m];
+    if (w >= a.part_total) return;
+    int lo_m = 0, hi_m = a.mesh_count - 1;  // last mesh with part_first <= w
+    while (lo_m < hi_m) {
+        const int c = (lo_m + hi_m + 1) >> 1;
+        if (a.meshes[c].part_first <= w) lo_m = c; else hi_m = c - 1;
+    }
+    const MeshSrcDev M = a.meshes[lo_m];
+    const int v0 = (w - M.part_first) * kAabbPart, v1 = min(M.vertex_count, v0 + kAabbPart);
     float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-    for (int v = lane; v < M.vertex_count; v += rtd::kWaveSize) {
+    for (int v = v0 + lane; v < v1; v += rtd::kWaveSize) {
         const float *p = a.world + 3 * (size_t)(M.vertex_first + v);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -74,9 +82,23 @@ __global__ void k_aabbs(XformArgs a) {
         hi[c] = wave_max(hi[c]);
     }
     if (lane == 0) {
-        a.aabbs[m].lo = make_float4(lo[0], lo[1], lo[2], 0.0f);
-        a.aabbs[m].hi = make_float4(hi[0], hi[1], hi[2], 0.0f);
+        a.parts[w].lo = make_float4(lo[0], lo[1], lo[2], 0.0f);
+        a.parts[w].hi = make_float4(hi[0], hi[1], hi[2], 0.0f);
     }
+}
+
+__global__ void k_aabbs(XformArgs a) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= a.mesh_count) return;
+    const int p0 = a.meshes[m].part_first, p1 = m + 1 < a.mesh_count ? a.meshes[m + 1].part_first : a.part_total;
+    float4 lo = a.parts[p0].lo, hi = a.parts[p0].hi;
+    for (int p = p0 + 1; p < p1; ++p) {
+        const float4 l = a.parts[p].lo, h = a.parts[p].hi;
+        lo = make_float4(rtm::umin(l.x, lo.x), rtm::umin(l.y, lo.y), rtm::umin(l.z, lo.z), 0.0f);
+        hi = make_float4(rtm::umax(h.x, hi.x), rtm::umax(h.y, hi.y), rtm::umax(h.z, hi.z), 0.0f);
+    }
+    a.aabbs[m].lo = lo;
+    a.aabbs[m].hi = hi;
 }
 
 // Triangles from the index buffer in order; mesh normal = -Triangle.Normal.
@@ -107,8 +129,9 @@ hipError_t transform_meshes(const XformArgs &a, hipStream_t stream) {
         hipLaunchKernelGGL(k_vertices, dim3((a.vertex_total + kThreads - 1) / kThreads), dim3(kThreads), 0, stream,
                            a);
     const int waves_per_block = kThreads / rtd::kWaveSize;
-    hipLaunchKernelGGL(k_aabbs, dim3((a.mesh_count + waves_per_block - 1) / waves_per_block), dim3(kThreads), 0,
+    hipLaunchKernelGGL(k_aabb_parts, dim3((a.part_total + waves_per_block - 1) / waves_per_block), dim3(kThreads), 0,
                        stream, a);
+    hipLaunchKernelGGL(k_aabbs, dim3((a.mesh_count + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, a);
     if (a.tri_total > 0)
         hipLaunchKernelGGL(k_triangles, dim3((a.tri_total + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, a);
     return hipGetLastError();
