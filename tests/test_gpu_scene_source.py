@@ -69,6 +69,26 @@ def test_mixed_sources_equal_host_extraction(gpu_ctx, rt, orc):
     assert _counts(sa) == (counts["primary_rays"], counts["shadow_rays"], counts["reflection_rays"])
 
 
+def test_big_mesh_aabb_in_parts(gpu_ctx, rt, orc):
+    """C3's 35k-vertex knot as one source mesh: its Mesh.AABB is reduced over
+    18 parts of 2,048 vertices (scene_xform.hip k_aabb_parts) and must give
+    the host extraction's frame and the oracle's."""
+    S = rt.scenes
+    fr0 = rt.make("C3").with_resolution(96, 54)
+    base = S.without_meshes(fr0.scene)
+    verts, idx = S.torus_knot()
+    assert len(verts) > 16 * 2048
+    srcs = [rt.MeshSource(verts, idx, np.eye(4, dtype=np.float32), S.KNOT_MAT)]
+    host = S.extracted(fr0.with_(scene=base), srcs)
+    gpu_ctx.set_scene_source(base, srcs)
+    a, sa = gpu_ctx.render(host.camera, host.plane, rt.frame_params(host))
+    gpu_ctx.set_scene(host.scene, 0)
+    b, sb = gpu_ctx.render(host.camera, host.plane, rt.frame_params(host))
+    assert _same(a, b) and _counts(sa) == _counts(sb)
+    ref, counts = orc.render(host)
+    assert float(np.max(np.abs(a - ref))) <= TOL
+
+
 def test_intersect_on_device_extracted_geometry(gpu_ctx, rt, orc):
     """Hit distances are bit-exact, so the device's world-space vertices equal
     the host's MultiplyPoint3x4 results."""
