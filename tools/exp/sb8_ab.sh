@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+for k in 1 2; do
+for v in default sorted; do
+L=""; [ $v != default ] && L="--lib $v"
+timeout -k 10 200 python bench.py --steps 100 --warmup 5 --no-cpu-baseline --sim-bands 8 $L > gpurun_out/sbx_${v}_$k.log 2>&1 || exit 1
+grep -v amdgpu gpurun_out/sbx_${v}_$k.log | tail -1 | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$v', $k, round(d['value']), d['ms_per_step'])"
+done; done

@@ -182,11 +182,28 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                     if (COUNT) cnt.box += 4;
                 }
             }
-            // wave-wide order: children nobody needs get +inf; the others are
-            // ordered by the entry distance of a representative live lane
-            // (children it misses go last).  Order only affects speed.  Keys
-            // are >= 0, so their bit patterns order as unsigned integers and
-            // the whole ordering runs on the scalar unit.
+            if (ANY) {
+                // any-hit (shadow rays): the order cannot change the answer,
+                // so the children any live lane needs are taken in slot order
+                // without the wave-wide sort (C3 -6 %, C2 -3 %, C5 +-0)
+                const bool n0 = __ballot(k0 != INFINITY) != 0, n1 = __ballot(k1 != INFINITY) != 0,
+                           n2 = __ballot(k2 != INFINITY) != 0, n3 = __ballot(k3 != INFINITY) != 0;
+                int nn = 0, nxt = 0;
+                if (n3) { nxt = ch.w; ++nn; }
+                if (n2) { if (nn) RT_PK_PUSH(nxt); nxt = ch.z; ++nn; }
+                if (n1) { if (nn) RT_PK_PUSH(nxt); nxt = ch.y; ++nn; }
+                if (n0) { if (nn) RT_PK_PUSH(nxt); nxt = ch.x; ++nn; }
+                if (nn) {
+                    node = uni(nxt);
+                    continue;
+                }
+            } else {
+            // closest hit, wave-wide order: children nobody needs get +inf;
+            // the others are ordered by the entry distance of a
+            // representative live lane (children it misses go last).  Order
+            // only affects speed.  Keys are >= 0, so their bit patterns order
+            // as unsigned integers and the whole ordering runs on the scalar
+            // unit.
             const unsigned long long live_m = __ballot(L.live);
             const int rep = __ffsll((long long)live_m) - 1;
             unsigned q0 = wave_key_bits(k0, rep), q1 = wave_key_bits(k1, rep), q2 = wave_key_bits(k2, rep),
@@ -214,6 +231,7 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                 if (q1 != kKeyNone) RT_PK_PUSH(c1);
                 node = uni(c0);
                 continue;
+            }
             }
         } else {
             const int v = ~node;
