@@ -73,12 +73,13 @@ def lib_sha256(path):
     return h.hexdigest()
 
 
-def load_pmc(config, lib_path):
+def load_pmc(config, lib_path, bands=1):
     """Per-launch PMC counters of the trace kernel (profiles/pmc_<config>.json,
+    or pmc_<config>_b<N>.json for one rank's row band of an N-GPU frame;
     written by tools/pmc_round.sh + tools/pmc_summary.py on the GPU box).  Used
     only when it was measured with the library this run loads (sha256 of the
     .so), so the counters describe the code that ran."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    p = os.path.join(ROOT, "profiles", f"pmc_{config}.json" if bands <= 1 else f"pmc_{config}_b{bands}.json")
     if not os.path.exists(p):
         return None, "missing"
     try:
@@ -129,6 +130,29 @@ def roofline(pmc, pmc_state, kernel_name, avg_kernel_s, logical):
     else:  # no counters for this build: the HBM leg cannot be priced
         out.update({"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None})
     return out
+
+
+def trace_kernel_name(mode, spp, depth, res_x, local_rows):
+    """The trace kernel instance a frame launches (rtk::launch_render_mega and
+    lpt_prepare in csrc/trace.hip / csrc/rt_abi.cpp): the all-packet levels
+    kernel for >= 16 spp, otherwise render_kernel<COUNT, SPLIT, DEEP, Q4> —
+    SPLIT when a frame or shard is small enough to split its slowest tiles
+    (<= 24,000 tiles, or <= 70,000 for sixteenth-waves only), Q4 for 2x2 spp."""
+    if mode == "packet":
+        return "render_packet_kernel<false, true>"
+    if mode == "wavefront":
+        return "wavefront passes (sum)"
+    deep = depth > 32  # rtd::kMaxBounces
+    if spp >= 16 and not deep:
+        return "render_levels_kernel"
+    ppw = 64 // spp
+    lg = ppw.bit_length() - 1
+    th = 1 << (lg // 2) if ppw & (ppw - 1) == 0 else 1
+    tw = ppw // th
+    tiles = -(-res_x // tw) * -(-local_rows // th)
+    split = not deep and ((16 % spp == 0 and tiles <= 24000) or (4 % spp == 0 and tiles <= 70000))
+    b = lambda v: "true" if v else "false"  # noqa: E731
+    return f"render_kernel<false, {b(split)}, {b(deep)}, {b(spp == 4 and tw == 4 and th == 4 and not deep)}>"
 
 
 def host_facts():
@@ -581,11 +605,8 @@ def main():
 
     if rank == 0:
         avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's own trace kernel, HIP events
-        pmc, pmc_state = load_pmc(args.config, lib_path)
-        # the megakernel instance the frame ran: <COUNT, SPLIT, DEEP, Q4>, Q4 for 2x2 spp (4x4-pixel tiles)
-        q4 = "true" if fr.spp == 4 else "false"
-        kname = {"megakernel": f"render_kernel<false, false, false, {q4}>",
-                 "packet": "render_packet_kernel<false, true>"}.get(args.mode, "wavefront passes (sum)")
+        pmc, pmc_state = load_pmc(args.config, lib_path, band_count)
+        kname = trace_kernel_name(args.mode, fr.spp, fr.max_bounces, rx, local_rows)
         rays_per_frame = rays // args.steps
         line = {
             "metric": METRIC,

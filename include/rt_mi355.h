@@ -180,7 +180,9 @@ typedef struct rt_stats {
     double total_ms;           /* wall time of the whole call                     */
     uint64_t primary_scene_misses; /* camera samples rejected by the Scene.AABB gate
                                       (Scene.cs:54) before any object test
-                                      (RT_FLAG_COUNT_TESTS)                         */
+                                      (RT_FLAG_COUNT_TESTS frames of the default
+                                      megakernel path only; 0 when the frame also
+                                      sets RT_FLAG_PACKET or RT_FLAG_WAVEFRONT)      */
     uint64_t shadow_rays_moot; /* shadow rays (counted in shadow_rays) whose answer
                                   cannot change the pixel — the light's unoccluded
                                   term leaves the colour's bits unchanged, e.g. a

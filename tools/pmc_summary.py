@@ -41,6 +41,8 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--kernel", default="render_kernel<false>")
     ap.add_argument("--out", default="")
+    ap.add_argument("--config", default="", help="recorded: the config the counters were taken on")
+    ap.add_argument("--bands", type=int, default=1, help="recorded: row band 0 of N (one rank's share)")
     ap.add_argument("--lib", default=os.path.join(ROOT, "unity-raytracer_amd", "lib", "librt_mi355.so"),
                     help="the library the counters were measured with (its sha256 is recorded; bench.py uses "
                          "the counters only with the same build)")
@@ -50,7 +52,7 @@ def main():
     for k, cs in vals.items():
         summary[k] = {c: sum(v) / len(v) for c, v in cs.items()}
     pick = {k: v for k, v in summary.items() if a.kernel in k}
-    res = {"kernels": summary}
+    res = {"kernels": summary, "config": a.config or None, "bands": a.bands}
     if pick:
         name, c = max(pick.items(), key=lambda kv: len(kv[1]))
         rd = None

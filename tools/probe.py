@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--bounces", type=int, default=-99)
     ap.add_argument("--no-lights", action="store_true")
     ap.add_argument("--band", default="", help="i/n: render only row band i of n (8-row blocks): a light load")
+    ap.add_argument("--rgb32f", action="store_true", help="float RGB output (the bench's shard format at N > 1)")
     a = ap.parse_args()
     rt = _rt_pkg.load()
     fr = rt.make(a.config)
@@ -58,6 +59,8 @@ def main():
         for mode in a.modes.split(","):
             flags = {"wavefront": rt.abi.RT_FLAG_WAVEFRONT, "packet": rt.abi.RT_FLAG_PACKET,
                      "rowmajor": rt.abi.RT_FLAG_ROW_ORDER}.get(mode, 0)
+            if a.rgb32f:
+                flags |= rt.abi.RT_FLAG_OUT_RGB32F
             bkw = {}
             if a.band:
                 bi, bn = map(int, a.band.split("/"))

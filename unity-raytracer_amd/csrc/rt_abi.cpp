@@ -138,10 +138,36 @@ Rccl &rccl() {
     return r;
 }
 
-// roctx ranges around the host-side phases (visible in rocprofv3 --marker-trace).
+// roctx ranges around the host-side phases (visible in rocprofv3
+// --marker-trace).  The roctx library is resolved lazily like RCCL, so a host
+// whose loader path lacks it still loads this library (ranges become no-ops).
+struct Roctx {
+    decltype(&roctxRangePushA) push = nullptr;
+    decltype(&roctxRangePop) pop = nullptr;
+};
+
+const Roctx &roctx() {
+    static const Roctx r = [] {
+        Roctx x;
+        void *h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            x.push = (decltype(x.push))dlsym(h, "roctxRangePushA");
+            x.pop = (decltype(x.pop))dlsym(h, "roctxRangePop");
+            if (!x.push || !x.pop) x.push = nullptr, x.pop = nullptr;
+        }
+        return x;
+    }();
+    return r;
+}
+
 struct Range {
-    explicit Range(const char *name) { roctxRangePushA(name); }
-    ~Range() { roctxRangePop(); }
+    explicit Range(const char *name) {
+        if (roctx().push) roctx().push(name);
+    }
+    ~Range() {
+        if (roctx().pop) roctx().pop();
+    }
 };
 
 }  // namespace
@@ -865,7 +891,8 @@ int run_lbvh(rt_ctx *ctx, const rtl::LbvhInput &in, bool wide, rtd::SceneDev &S,
     // traversal stack: one entry per 2-wide level, three per 4-wide level
     const int need = wide ? 3 * (binfo[2] + 1) : binfo[0] + 1;
     if (need > rtd::kStackTotal)
-        return fail(ctx, RT_E_SCENE, "LBVH depth %d exceeds the traversal stack; use RT_BUILD_SAH_HOST", binfo[0]);
+        return fail(ctx, RT_E_SCENE, "LBVH %d-wide depth %d exceeds the traversal stack; use RT_BUILD_SAH_HOST",
+                    wide ? 4 : 2, wide ? binfo[2] : binfo[0]);
     S.nodes = (const rtd::BvhNode *)B.nodes.p;
     S.nodes4 = wide ? (const rtd::BvhNode4 *)B.nodes4.p : nullptr;
     S.tris = (const rtd::TriRec *)B.tris.p;
@@ -1069,10 +1096,12 @@ int for_members(rt_ctx *ctx, Fn fn) {
 }
 
 void release_group(rt_ctx *ctx) {
-    Rccl &R = rccl();
-    for (ncclComm_t c : ctx->comms)
-        if (c && R.ok) (void)R.comm_destroy(c);
-    ctx->comms.clear();
+    if (!ctx->comms.empty()) {  // only an RCCL group ever loaded the library
+        Rccl &R = rccl();
+        for (ncclComm_t c : ctx->comms)
+            if (c && R.ok) (void)R.comm_destroy(c);
+        ctx->comms.clear();
+    }
     const int n = nmembers(ctx);
     for (GroupSlot &g : ctx->gslots) {
         if (!g.used) continue;

@@ -112,7 +112,9 @@ __device__ __noinline__ f3 deep_chain(const SceneDev &S, const FrameDev &F, f3 o
     {
         f3 o = oc, d = dc;
         while (true) {
-            const int k = walk_level<COUNT>(S, F, o, d, end, st, cnt, sf);
+            // the level-lc ray was traversed and counted by the caller: walk it
+            // again without counting its tests and its shading fetch
+            const int k = walk_level<COUNT>(S, F, o, d, end, st, end == lc ? none : cnt, sf);
             if (k == 0) {
                 term = rtt::ld3(F.bg255);  // :310-311
                 break;
@@ -183,7 +185,6 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
         if (COUNT) cnt.shading++;
         const rts::Surface sf = rts::surface(S, o, d, bt, br);
         if (DEEP && depth - depth0 == kMaxBounces && S.mats[sf.mat].ka_mirror.w != 0.0f && depth < F.max_bounces) {
-            if (COUNT) cnt.shading--;  // deep_chain counts this hit again
             return deep_chain<COUNT>(S, F, o0, d0, depth0, o, d, st, cnt);
         }
         const f3 col = shade_hit<COUNT>(S, sf, st, cnt);
