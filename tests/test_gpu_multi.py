@@ -41,8 +41,35 @@ def test_group_frame_bit_identical(gpu_ctx, rt, devices, gather):
             assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), (name, devices, gather)
             assert _rays(st) == _rays(sref), (name, devices)
             assert st.kernel_ms > 0
+            # the device-output path gathers the bands (RCCL / peer copies) and reassembles
+            H, W = fr.plane.ResolutionY, fr.plane.ResolutionX
+            dev = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+            st2 = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr), dev.data_ptr(), dev.numel() * 4)
+            assert np.array_equal(dev.cpu().numpy().view(np.uint32), ref.view(np.uint32)), (name, devices, "device")
+            assert _rays(st2) == _rays(sref)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_group_host_frame_direct_band_copies(gpu_ctx, rt, n):
+    """rt_render on a group: every member copies its own row blocks into the
+    caller's frame (one 2-D copy + a last partial block), in every pixel
+    format, for heights that end in a partial 8-row block and for members
+    that own no block at all."""
+    for res in ((97, 61), (64, 8), (40, 3), (250, 131)):
+        fr = _frame(rt, "C3", res)
+        ctx = rt.Context(devices=[0] * n, gather=1)
+        try:
+            ctx.set_scene(fr.scene)
+            for flags in (0, rt.abi.RT_FLAG_OUT_RGBA8, rt.abi.RT_FLAG_OUT_RGB32F, rt.abi.RT_FLAG_OUT_RGBA16F):
+                ref, sref = _single(gpu_ctx, rt, fr, flags)
+                img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=flags))
+                assert img.shape == ref.shape
+                assert np.array_equal(img.view(np.uint8), ref.view(np.uint8)), (res, n, flags)
+                assert _rays(st) == _rays(sref), (res, n, flags)
+        finally:
+            ctx.close()
 
 
 def test_group_output_formats_and_device_output(gpu_ctx, rt):

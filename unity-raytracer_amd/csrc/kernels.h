@@ -12,6 +12,8 @@ namespace rtk {
 // Megakernel: one lane per sample, whole Whitted chain in one launch (trace.hip).
 // Longest-first tile order for the next frame (trace.hip).
 size_t tile_sort_scratch_bytes(int n);
+// waves of a render_kernel launch of F (tiles + the extra waves of split tiles)
+int render_mega_waves(const rtd::FrameDev &F);
 hipError_t launch_iota(int *p, int n, hipStream_t stream);
 hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const int *iota, int *order, int n,
                               void *scratch, size_t scratch_bytes, hipStream_t stream);

@@ -65,12 +65,13 @@ struct LptSlot {
     int slab = 0;  // rt_render row slab (0 for whole frames)
     bool used = false;
     GrowBuf cost, cost_sorted, iota, order, scratch;
+    GrowBuf wave_counts;  // render_kernel's per-wave ray tallies (rtd::FrameDev::wave_counts)
     long long key = -1;
     unsigned long long scene = ~0ull;
     bool valid = false;
     long long frames = 0;
     void release() {
-        for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch}) {
+        for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch, &wave_counts}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;
@@ -345,6 +346,44 @@ int32_t band_local_rows(int32_t res_y, int32_t band_count, int32_t band_rows) {
     return slots * band_rows;
 }
 
+// The conservative sky test's per-frame constants (rt_device.h FrameDev
+// sky_*), in double: the Scene.AABB padded by 2^-10 of the camera-relative
+// scene scale.  An exact sample ray that passes the exact gate (RMath.cs:12-26)
+// comes geometrically within ~1e-7 of that scale of the box; the kernel's
+// approximate ray deviates by ~1e-6 of it; the pad is ~1e-3 of it.  Off when
+// anything is non-finite or the camera is inside the padded box (every ray
+// may then enter it).
+void sky_setup(const rtd::SceneDev &S, rtd::FrameDev &F) {
+    F.sky_test = 0;
+    if (!S.has_prims || F.res_x <= 0 || F.res_y <= 0) return;
+    double lo[3], hi[3], c[3], scale = 0.0;
+    bool finite = std::isfinite(F.hl) && std::isfinite(F.vl);
+    for (int a = 0; a < 3; ++a) {
+        c[a] = F.cam_pos[a];
+        lo[a] = (double)S.scene_lo[a] - c[a];
+        hi[a] = (double)S.scene_hi[a] - c[a];
+        finite = finite && std::isfinite(lo[a]) && std::isfinite(hi[a]) && lo[a] <= hi[a] &&
+                 std::isfinite(F.top_left[a]) && std::isfinite(F.right[a]) && std::isfinite(F.up[a]);
+        scale = std::max(scale, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+    }
+    if (!finite) return;
+    const double pad = std::ldexp(std::max(scale, 1e-30), -10);
+    bool inside = true;
+    for (int a = 0; a < 3; ++a) {
+        lo[a] -= pad;
+        hi[a] += pad;
+        inside = inside && lo[a] <= 0.0 && hi[a] >= 0.0;
+        F.sky_lo[a] = (float)lo[a];
+        F.sky_hi[a] = (float)hi[a];
+        F.sky_tlc[a] = (float)((double)F.top_left[a] - c[a]);
+    }
+    if (inside) return;
+    // rounding the padded bounds to float moves them by far less than the pad
+    F.sky_hx = (float)((double)F.hl / F.res_x);
+    F.sky_vy = (float)((double)F.vl / F.res_y);
+    F.sky_test = 1;
+}
+
 int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, const rt_render_params *prm,
                   rtd::FrameDev &F, size_t &out_bytes) {
     if (!cam || !plane || !prm) return fail(ctx, RT_E_INVALID, "null camera/plane/params");
@@ -402,6 +441,7 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
         return fail(ctx, RT_E_INVALID, "RT_FLAG_OUT_RGBA8, RT_FLAG_OUT_RGBA16F and RT_FLAG_OUT_RGB32F are exclusive");
     F.out_format = f8 ? rtd::kOutRGBA8 : (f16 ? rtd::kOutRGBA16F : (f12 ? rtd::kOutRGB32F : rtd::kOutFloat4));
     out_bytes = (size_t)F.local_rows * F.res_x * rt_pixel_bytes(prm->flags);
+    sky_setup(ctx->S, F);
     return RT_OK;
 }
 
@@ -597,6 +637,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     lpt_sort = false;
     F.tile_order = nullptr;
     F.tile_cost = nullptr;
+    F.wave_counts = nullptr;
     if (!mega || (prm->flags & RT_FLAG_ROW_ORDER) != 0 || F.num_tiles <= 0) return RT_OK;
     for (LptSlot &l : ctx->lpt)
         if (l.used && l.stream == ctx->stream && l.slab == slab) ls = &l;
@@ -651,6 +692,13 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
                F.num_tiles <= kSplit16MaxTiles) {
         F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
+    }
+    // render_kernel's ray tallies: one plain store per wave into this slot's
+    // buffer, reduced after the launch on the same stream (an atomic per wave
+    // holds the wave's slot for its round trip: C2 -13 %, C3 -4 %)
+    if (!count && !(ctx->S.bvh4 && F.spp >= 16)) {
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->wave_counts, (size_t)rtk::render_mega_waves(F) * sizeof(uint4)));
+        F.wave_counts = (uint4 *)ls->wave_counts.p;
     }
     return RT_OK;
 }
@@ -709,6 +757,65 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         int st = prepare_wavefront(ctx, F, chunk_tiles, A);
         if (st) return st;
     }
+    // rt_render into a host Color[]: the frame in row slabs, each copied to the
+    // host while the next ones render (the PCIe copy is the longer part)
+    const bool slabs = host_out && out_bytes && F.band_count == 1 && !P.wavefront;
+    struct Launch {
+        rtd::FrameDev F;
+        LptSlot *ls;
+        bool sort;
+        hipStream_t stream;
+        int r0, r1;
+    };
+    std::vector<Launch> launches;
+    const hipStream_t base = ctx->stream;
+    struct Restore {
+        rt_ctx *c;
+        hipStream_t s;
+        ~Restore() { c->stream = s; }
+    } restore{ctx, base};
+    int row_bytes = 0;
+    // every launch's longest-first state first (its first use allocates):
+    // outside the timed region, which covers device work only
+    if (slabs) {
+        row_bytes = (int)(out_bytes / (size_t)std::max(1, F.local_rows));
+        const int nslab = std::max(1, std::min(kMaxSlabs, (int)(out_bytes / kSlabBytes)));
+        // slab boundaries on whole tile rows
+        const int tile_rows = (F.local_rows + F.tile_h - 1) / F.tile_h;
+        if (!ctx->copy_stream) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+        while ((int)ctx->slab_done.size() < nslab) {
+            hipEvent_t e;
+            HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ctx->slab_done.push_back(e);
+        }
+        // slabs alternate between two streams, so a slab's tail overlaps the
+        // next slab instead of idling the GPU
+        if (!ctx->slab_stream2) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->slab_stream2, hipStreamNonBlocking));
+        for (int k = 0; k < nslab; ++k) {
+            Launch L{};
+            L.stream = ctx->stream = (k & 1) ? ctx->slab_stream2 : base;
+            L.r0 = std::min(F.local_rows, (int)((long long)tile_rows * k / nslab) * F.tile_h);
+            L.r1 = std::min(F.local_rows, (int)((long long)tile_rows * (k + 1) / nslab) * F.tile_h);
+            L.F = F;
+            L.F.row0 = L.r0;
+            L.F.local_rows = L.r1 - L.r0;
+            L.F.num_tiles = L.F.res_x > 0 ? L.F.tiles_x * ((L.F.local_rows + L.F.tile_h - 1) / L.F.tile_h) : 0;
+            L.F.out = (char *)d_out + (size_t)L.r0 * row_bytes;
+            int st = lpt_prepare(ctx, L.F, prm, P.mega, P.count, k, L.ls, L.sort);
+            if (st) return st;
+            launches.push_back(L);
+        }
+        ctx->stream = base;
+    } else {
+        // megakernel frames dispatch a previous frame's most expensive tiles
+        // first (a frame's tail is its slowest tiles); the order is kept per stream
+        Launch L{};
+        L.F = F;
+        L.stream = base;
+        int st = lpt_prepare(ctx, L.F, prm, P.mega, P.count, 0, L.ls, L.sort);
+        if (st) return st;
+        launches.push_back(L);
+    }
     const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
     if (!async || ctx->async_frames == 0) {
         // async frames share one set of counters until rt_finish / the next synchronous frame
@@ -719,66 +826,30 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         // frames): it must not count before the counters were zeroed
         HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_a0, 0));
     }
-    // rt_render into a host Color[]: the frame in row slabs, each copied to the
-    // host while the next ones render (the PCIe copy is the longer part)
-    const bool slabs = host_out && out_bytes && F.band_count == 1 && !P.wavefront;
     if (slabs) {
-        const int row_bytes = (int)(out_bytes / (size_t)std::max(1, F.local_rows));
-        const int nslab = std::max(1, std::min(kMaxSlabs, (int)(out_bytes / kSlabBytes)));
-        // slab boundaries on whole tile rows
-        const int tile_rows = (F.local_rows + F.tile_h - 1) / F.tile_h;
-        if (!ctx->copy_stream) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
-        while ((int)ctx->slab_done.size() < nslab) {
-            hipEvent_t e;
-            HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            ctx->slab_done.push_back(e);
-        }
-        const rtd::FrameDev F0 = F;
-        std::vector<std::pair<LptSlot *, rtd::FrameDev>> sorts;
-        std::vector<hipStream_t> sort_streams;
-        std::vector<std::pair<int, int>> bounds;
-        // slabs alternate between two streams, so a slab's tail overlaps the
-        // next slab instead of idling the GPU
-        const hipStream_t base = ctx->stream;
-        if (!ctx->slab_stream2) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->slab_stream2, hipStreamNonBlocking));
+        const int nslab = (int)launches.size();
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_slab0, base));
         HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->slab_stream2, ctx->ev_slab0, 0));
-        struct Restore { rt_ctx *c; hipStream_t s; ~Restore() { c->stream = s; } } restore{ctx, base};
         for (int k = 0; k < nslab; ++k) {
-            ctx->stream = (k & 1) ? ctx->slab_stream2 : base;
-            const int r0 = std::min(F0.local_rows, (int)((long long)tile_rows * k / nslab) * F0.tile_h);
-            const int r1 = std::min(F0.local_rows, (int)((long long)tile_rows * (k + 1) / nslab) * F0.tile_h);
-            rtd::FrameDev Fk = F0;
-            Fk.row0 = r0;
-            Fk.local_rows = r1 - r0;
-            Fk.num_tiles = Fk.res_x > 0 ? Fk.tiles_x * ((Fk.local_rows + Fk.tile_h - 1) / Fk.tile_h) : 0;
-            Fk.out = (char *)d_out + (size_t)r0 * row_bytes;
-            LptSlot *ls = nullptr;
-            bool lpt_sort = false;
-            int st = lpt_prepare(ctx, Fk, prm, P.mega, P.count, k, ls, lpt_sort);
-            if (st) return st;
-            st = launch_frame(ctx, Fk, P, A, chunk_tiles);
+            ctx->stream = launches[k].stream;
+            int st = launch_frame(ctx, launches[k].F, P, A, chunk_tiles);
             if (st) return st;
             HIP_OR_FAIL(ctx, hipEventRecord(ctx->slab_done[k], ctx->stream));
-            if (lpt_sort) {
-                sorts.emplace_back(ls, Fk);
-                sort_streams.push_back(ctx->stream);
-            }
-            bounds.emplace_back(r0, r1);
         }
         ctx->stream = base;
         if (nslab > 1) HIP_OR_FAIL(ctx, hipStreamWaitEvent(base, ctx->slab_done[nslab - (nslab & 1 ? 2 : 1)], 0));
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, base));
-        for (size_t i = 0; i < sorts.size(); ++i) {  // after the timed region: the order of the next frames
-            ctx->stream = sort_streams[i];
-            int st = lpt_sort_now(ctx, sorts[i].second, sorts[i].first);
+        for (Launch &L : launches) {  // after the timed region: the order of the next frames
+            if (!L.sort) continue;
+            ctx->stream = L.stream;
+            int st = lpt_sort_now(ctx, L.F, L.ls);
             if (st) return st;
         }
         ctx->stream = base;
         // every launch is enqueued before the first copy: a copy into pageable
         // memory may hold the host until it is done
         for (int k = 0; k < nslab; ++k) {
-            const int r0 = bounds[k].first, r1 = bounds[k].second;
+            const int r0 = launches[k].r0, r1 = launches[k].r1;
             if (r1 <= r0) continue;
             HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->copy_stream, ctx->slab_done[k], 0));
             HIP_OR_FAIL(ctx, hipMemcpyAsync((char *)host_out + (size_t)r0 * row_bytes,
@@ -787,17 +858,12 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         }
         HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->copy_stream));
     } else {
-        // megakernel frames dispatch a previous frame's most expensive tiles
-        // first (a frame's tail is its slowest tiles); the order is kept per stream
-        LptSlot *ls = nullptr;
-        bool lpt_sort = false;
-        int st = lpt_prepare(ctx, F, prm, P.mega, P.count, 0, ls, lpt_sort);
-        if (st) return st;
-        st = launch_frame(ctx, F, P, A, chunk_tiles);
+        Launch &L = launches[0];
+        int st = launch_frame(ctx, L.F, P, A, chunk_tiles);
         if (st) return st;
         if (async) {
-            if (lpt_sort) {
-                st = lpt_sort_now(ctx, F, ls);
+            if (L.sort) {
+                st = lpt_sort_now(ctx, L.F, L.ls);
                 if (st) return st;
             }
             st = record_async_end(ctx);
@@ -810,8 +876,8 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             return RT_OK;
         }
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-        if (lpt_sort) {  // after the timed region: the order of the next frames
-            st = lpt_sort_now(ctx, F, ls);
+        if (L.sort) {  // after the timed region: the order of the next frames
+            st = lpt_sort_now(ctx, L.F, L.ls);
             if (st) return st;
         }
         if (host_out && out_bytes)
@@ -1252,6 +1318,53 @@ int take_async(rt_ctx *m, unsigned long long counts[rtd::kCounterWords], double 
     return RT_OK;
 }
 
+// A synchronous group frame's stats: every member's counters summed, the
+// slowest member's kernel time.
+int group_stats(rt_ctx *ctx, const std::vector<AsyncStash> &stash, rt_stats *stats,
+                std::chrono::steady_clock::time_point t0) {
+    unsigned long long sum[rtd::kCounterWords] = {0};
+    double kms = 0.0;
+    for (int i = 0; i < nmembers(ctx); ++i) {
+        rt_ctx *m = member(ctx, i);
+        unsigned long long c[rtd::kCounterWords];
+        double ms = 0.0;
+        const int st = take_async(m, c, ms);
+        unstash_async(m, stash[(size_t)i]);
+        if (st) {
+            if (i) ctx->err = m->err;
+            return st;
+        }
+        for (int w = 0; w < rtd::kCounterWords; ++w) sum[w] += c[w];
+        kms = std::max(kms, ms);
+    }
+    if (stats)
+        fill_stats(stats, sum, kms,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    return RT_OK;
+}
+
+// Member `band` of `bands` copies its compact band (block-cyclic R-row
+// blocks: local slot k holds image block k * bands + band) straight into the
+// caller's host frame on its own stream: one 2-D copy for the whole blocks
+// (source pitch = destination width = R rows, destination pitch = bands * R
+// rows) plus the rows of a last partial block.
+int copy_band_rows(rt_ctx *m, const void *band_buf, void *host, int res_x, int res_y, int band, int bands, int R,
+                   int px_bytes) {
+    const size_t row = (size_t)res_x * px_bytes;
+    const int full = res_y / R;                                   // whole blocks of the image
+    const int mine = full > band ? (full - band + bands - 1) / bands : 0;  // ... that are this member's
+    if (mine > 0 && row > 0)
+        HIP_OR_FAIL(m, hipMemcpy2DAsync((char *)host + (size_t)band * R * row, (size_t)bands * R * row, band_buf,
+                                        (size_t)R * row, (size_t)R * row, (size_t)mine, hipMemcpyDeviceToHost,
+                                        m->stream));
+    const int rest = res_y - full * R;  // rows of a last partial block
+    if (rest > 0 && full % bands == band && row > 0)
+        HIP_OR_FAIL(m, hipMemcpyAsync((char *)host + (size_t)full * R * row,
+                                      (const char *)band_buf + (size_t)(full / bands) * R * row, (size_t)rest * row,
+                                      hipMemcpyDeviceToHost, m->stream));
+    return RT_OK;
+}
+
 // One frame on a multi-device context: member i renders row band i of N
 // (block-cyclic, 8-row blocks) on a stream of its own, the bands travel to
 // the root (RCCL send/recv in one group, or peer copies), the root puts them
@@ -1290,8 +1403,12 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
     // the root's band goes straight into the gather buffer unless it travels
     // through RCCL itself (a one-device RCCL context: self send/receive)
     const bool root_self_send = rccl_gather && n == 1;
+    // rt_render into the caller's host frame: every member copies its own
+    // row blocks straight into their rows over its own link (no gather, no
+    // reassembly, no single-link copy of the whole frame from the root)
+    const bool direct_host = host_out && full_bytes;
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    HIP_OR_FAIL(ctx, ensure(ctx, gs->gather, (size_t)n * shard));
+    if (!direct_host) HIP_OR_FAIL(ctx, ensure(ctx, gs->gather, (size_t)n * shard));
     for (int i = 0; i < n; ++i) {
         rt_ctx *m = member(ctx, i);
         HIP_OR_FAIL(ctx, hipSetDevice(m->device));
@@ -1301,7 +1418,7 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
             stash_async(m, stash[(size_t)i]);
         }
         void *out;
-        if (i == 0 && !root_self_send) {
+        if (i == 0 && !root_self_send && !direct_host) {
             out = gs->gather.p;
         } else {
             HIP_OR_FAIL(ctx, ensure(m, gs->member_out[(size_t)i], shard));
@@ -1318,6 +1435,22 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
             if (i) ctx->err = m->err;
             return st;
         }
+        if (direct_host) {
+            st = copy_band_rows(m, out, host_out, plane->resolution_x, plane->resolution_y, i, n, R, px_bytes);
+            if (st) {
+                if (i) ctx->err = m->err;
+                return st;
+            }
+        }
+    }
+    if (direct_host) {
+        for (int i = 0; i < n; ++i) {
+            rt_ctx *m = member(ctx, i);
+            HIP_OR_FAIL(ctx, hipSetDevice(m->device));
+            HIP_OR_FAIL(ctx, hipStreamSynchronize(m->stream));
+        }
+        HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+        return group_stats(ctx, stash, stats, t0);
     }
     // gather the bands to the root
     if (rccl_gather) {
@@ -1361,25 +1494,7 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
         return RT_OK;
     }
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
-    unsigned long long sum[rtd::kCounterWords] = {0};
-    double kms = 0.0;
-    for (int i = 0; i < n; ++i) {
-        rt_ctx *m = member(ctx, i);
-        unsigned long long c[rtd::kCounterWords];
-        double ms = 0.0;
-        st = take_async(m, c, ms);
-        unstash_async(m, stash[(size_t)i]);
-        if (st) {
-            if (i) ctx->err = m->err;
-            return st;
-        }
-        for (int w = 0; w < rtd::kCounterWords; ++w) sum[w] += c[w];
-        kms = std::max(kms, ms);
-    }
-    if (stats)
-        fill_stats(stats, sum, kms,
-                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-    return RT_OK;
+    return group_stats(ctx, stash, stats, t0);
 }
 
 }  // namespace
@@ -1898,8 +2013,8 @@ int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
         const size_t bytes = (size_t)plane->resolution_x * plane->resolution_y * rt_pixel_bytes(params->flags);
         if (bytes && !out_rgba) return fail(ctx, RT_E_INVALID, "out_rgba is null");
         HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-        HIP_OR_FAIL(ctx, ensure_out(ctx, bytes));
-        return group_frame(ctx, camera, plane, params, ctx->d_out, out_rgba, bytes, stats, t0);
+        // every member copies its own rows to the host: no root-side frame buffer
+        return group_frame(ctx, camera, plane, params, nullptr, out_rgba, bytes, stats, t0);
     }
     rtd::FrameDev F;
     size_t bytes = 0;

@@ -155,6 +155,26 @@ __host__ __device__ __forceinline__ unsigned tile_cost_key(unsigned long long c6
     return e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
 }
 
+// Camera samples a launch of F traces: every pixel of its rows that lies in
+// the image (slot_pixel's test), spp samples each.
+__host__ __device__ inline unsigned long long active_samples(int res_x, int res_y, int local_rows, int row0,
+                                                             int band_index, int band_count, int band_rows,
+                                                             int spp) {
+    long long rows = 0;
+    if (band_count > 1) {
+        for (int ly = 0; ly < local_rows; ly += band_rows) {
+            const int blk = ly / band_rows;
+            const long long gy0 = ((long long)blk * band_count + band_index) * band_rows;
+            const long long n = (long long)(local_rows - ly < band_rows ? local_rows - ly : band_rows);
+            rows += gy0 >= res_y ? 0 : (gy0 + n <= res_y ? n : res_y - gy0);
+        }
+    } else {
+        const long long end = (long long)row0 + local_rows;
+        rows = end <= res_y ? local_rows : (row0 < res_y ? res_y - row0 : 0);
+    }
+    return (unsigned long long)(rows > 0 ? rows : 0) * (unsigned long long)(res_x > 0 ? res_x : 0) * spp;
+}
+
 // Per-frame constants of CastPixelRays (RayTracingSetup.cs:277-284).
 struct FrameDev {
     float cam_pos[3];
@@ -178,6 +198,19 @@ struct FrameDev {
     int split16_tiles;       // render_kernel: the first split16_tiles of tile_order run as 16 sixteenth-waves each,
     int split_tiles;         // ... the next split_tiles as 4 quarter-waves each
     unsigned long long *counters;  // kCounterSlots x kCounterWords u64, rt_stats order
+    // Conservative sky test (render_kernel, non-counting instances): a wave
+    // whose every sample ray, approximated (relative error ~1e-6), misses the
+    // padded Scene.AABB (pad 2^-10 of the camera-relative scene scale, far
+    // above the approximation and rounding errors) is background without its
+    // exact rays: each of them misses the exact Scene.AABB gate (Scene.cs:54),
+    // so Shade returns the background (RayTracingSetup.cs:310-311).
+    unsigned long long primary_total;  // render_kernel (non-counting): camera samples of this launch, added once
+    uint4 *wave_counts;      // render_kernel (non-counting): per-wave {shadow, reflection, moot} tallies, one
+                             // uint4 per wave of the launch, reduced after it; null: per-wave atomics
+    int sky_test;            // 1: on (camera outside the padded box, all inputs finite)
+    float sky_tlc[3];        // top_left - cam_pos
+    float sky_hx, sky_vy;    // HorizontalLength / res_x, VerticalLength / res_y
+    float sky_lo[3], sky_hi[3];  // padded Scene.AABB - cam_pos
 };
 
 }  // namespace rtd

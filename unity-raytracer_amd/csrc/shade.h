@@ -139,6 +139,30 @@ __device__ __forceinline__ void primary_ray(const rtd::FrameDev &F, int px, int 
     d = rtm::normalize(pp - o);
 }
 
+// The conservative sky test of one sample (FrameDev sky_*, rt_abi.cpp
+// sky_setup): false only when the sample's ray, approximated with fast
+// reciprocals (relative error ~1e-6, far inside the pad), surely misses the
+// padded Scene.AABB — then the exact ray misses the exact gate (Scene.cs:54).
+// A NaN anywhere leaves the answer "maybe" (fminf/fmaxf ignore NaN operands).
+template <bool Q4 = false>
+__device__ __forceinline__ bool sky_maybe(const rtd::FrameDev &F, int px, int gy, int s) {
+    const int n = Q4 ? 2 : F.spp_n;
+    const int sj = Q4 ? s >> 1 : s / n, si = Q4 ? s & 1 : s - sj * n;
+    const float rn = Q4 ? 0.5f : __builtin_amdgcn_rcpf((float)n);
+    const float ax = ((float)px + ((float)si + 0.5f) * rn) * F.sky_hx;
+    const float ay = ((float)gy + ((float)sj + 0.5f) * rn) * F.sky_vy;
+    const float dx = F.sky_tlc[0] + ax * F.right[0] - ay * F.up[0];
+    const float dy = F.sky_tlc[1] + ax * F.right[1] - ay * F.up[1];
+    const float dz = F.sky_tlc[2] + ax * F.right[2] - ay * F.up[2];
+    const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy), iz = __builtin_amdgcn_rcpf(dz);
+    const float lx = F.sky_lo[0] * ix, hx = F.sky_hi[0] * ix;
+    const float ly = F.sky_lo[1] * iy, hy = F.sky_hi[1] * iy;
+    const float lz = F.sky_lo[2] * iz, hz = F.sky_hi[2] * iz;
+    const float tmin = fmaxf(fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fminf(lz, hz)), 0.0f);
+    const float tmax = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fmaxf(lz, hz));
+    return !(tmin > tmax);
+}
+
 // Sum of a pixel's samples in row-major sample order ((s0 + s1) + s2) + ...,
 // valid at the pixel's sample-0 lane (samples sit in consecutive lanes).  4
 // spp: DPP quad moves (no LDS round trip); otherwise lane shuffles.  Must be

@@ -228,10 +228,10 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
         const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
-        cnt.shadow++;
         // a moot shadow ray (shade.h same_bits) is not traced
         const f3 lit = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
         const bool moot = rts::same_bits(lit, col);
+        cnt.shadow++;
         cnt.moot += moot;
         rtt::RayCtx rs;
         rtt::setup_ray(rs, sr.o, sr.dir);
@@ -275,16 +275,27 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     const bool active =
         rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
     f3 color = mk(0.0f, 0.0f, 0.0f);
+    // a wave whose samples all surely miss the padded Scene.AABB is background
+    // without its exact rays (shade.h sky_maybe; the counting launch traces all)
+    bool sky = false;
+#ifndef RT_EXP_NOSKY
+    if (!COUNT) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4>(F, px, gy, s))) == 0;
+#endif
     if (active) {
-        f3 o, d;
-        rts::primary_ray<Q4>(F, px, gy, s, o, d);
-        cnt.primary += 1;
-        if (COUNT) {  // trivially cheap camera samples: they miss Scene.AABB (Scene.cs:54)
-            rtt::RayCtx rg;
-            rtt::setup_ray(rg, o, d);
-            cnt.scene_miss += !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
+        if (COUNT) cnt.primary += 1;  // otherwise F.primary_total, added once per launch
+        if (sky) {
+            color = rtt::ld3(F.bg255);  // :310-311
+        } else {
+            f3 o, d;
+            rts::primary_ray<Q4>(F, px, gy, s, o, d);
+            if (COUNT) {  // trivially cheap camera samples: they miss Scene.AABB (Scene.cs:54)
+                rtt::RayCtx rg;
+                rtt::setup_ray(rg, o, d);
+                cnt.scene_miss +=
+                    !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
+            }
+            color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg);
         }
-        color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg);
     }
     const f3 sum = rts::sample_sum(color, lane, F.spp);
     // the slot -> pixel mapping is recomputed from the (scalar) tile index
@@ -293,9 +304,15 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     asm volatile("" : "+s"(tile2));
     const bool active2 =
         rts::slot_pixel<Q4>(F, tile2, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
+#ifdef RT_EXP_SKYNOSTORE
+    if (sky) return;  // measurement only: what a sky wave's pixel store costs
+#endif
     if (active2 && s == 0) {
         f3 v = sum;
-        if (F.spp > 1) v = v / (float)F.spp;
+        if (Q4)
+            v = v * 0.25f;  // == v / 4: the same real number, rounded once
+        else if (F.spp > 1)
+            v = v / (float)F.spp;
         rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
     }
 }
@@ -336,6 +353,9 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
         const int w2 = wid - 15 * split16 - 3 * split;
         tile = F.tile_order ? rtt::cload(F.tile_order + w2) : w2;
     }
+    // the launch's camera samples (one per active lane of every tile, computed
+    // by the host: rt_device.h active_samples), counted once per launch
+    if (!COUNT && !F.wave_counts && wid == 0 && lane == 0) atomicAdd(rtt::counter_slot(F.counters), F.primary_total);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
@@ -372,7 +392,59 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     if (F.tile_cost && lane == 0 && part <= 0) {
         F.tile_cost[tile] = tile_cost_key(__builtin_amdgcn_s_memtime() - t0, part, pshift);
     }
-    rtt::flush_counts<COUNT>(cnt, F.counters);
+#ifndef RT_EXP_NOFLUSH
+    if (!COUNT && F.wave_counts) {
+        // the wave's tallies by a plain store (reduced by wave_counts_kernel
+        // after the launch): an atomic holds the wave's slot for its whole
+        // round trip, a store beside the pixel store costs next to nothing
+        unsigned sh = 0, rf = 0, mo = 0;
+        if (__ballot((cnt.shadow | cnt.reflection | cnt.moot) != 0) != 0) {
+            sh = rtt::wave_sum(cnt.shadow);
+            rf = rtt::wave_sum(cnt.reflection);
+            mo = rtt::wave_sum(cnt.moot);
+        }
+        if (lane == 0) F.wave_counts[wid] = make_uint4(sh, rf, mo, 0u);
+    } else {
+        rtt::flush_counts<COUNT>(cnt, F.counters);
+    }
+#endif
+}
+
+// Per-wave tallies of a render_kernel launch (F.wave_counts) -> the frame's
+// sharded counters: shadow, reflection and moot rays, plus the launch's
+// camera samples (F.primary_total) once.
+__global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n, unsigned long long primary_total,
+                                                         unsigned long long *counters) {
+    unsigned long long sh = 0, rf = 0, mo = 0;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const uint4 v = wc[i];
+        sh += v.x;
+        rf += v.y;
+        mo += v.z;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sh += __shfl_xor(sh, off);
+        rf += __shfl_xor(rf, off);
+        mo += __shfl_xor(mo, off);
+    }
+    __shared__ unsigned long long part[4][3];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        part[w][0] = sh;
+        part[w][1] = rf;
+        part[w][2] = mo;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long *ctr = counters + (size_t)(blockIdx.x % kCounterSlots) * kCounterWords;
+        const unsigned long long a = part[0][0] + part[1][0] + part[2][0] + part[3][0];
+        const unsigned long long b = part[0][1] + part[1][1] + part[2][1] + part[3][1];
+        const unsigned long long c = part[0][2] + part[1][2] + part[2][2] + part[3][2];
+        if (blockIdx.x == 0 && primary_total) atomicAdd(ctr + 0, primary_total);
+        if (a) atomicAdd(ctr + 1, a);
+        if (b) atomicAdd(ctr + 2, b);
+        if (c) atomicAdd(ctr + 8, c);
+    }
 }
 
 // Wave-synchronous megakernel: the Whitted chain advances level by level for
@@ -529,8 +601,11 @@ namespace rtk {
 constexpr int kLevelsMinSpp = 16;
 
 
-hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_tests, hipStream_t stream) {
-    if (F.num_tiles <= 0) return hipSuccess;
+hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_tests, hipStream_t stream) {
+    if (F0.num_tiles <= 0) return hipSuccess;
+    FrameDev F = F0;
+    F.primary_total = active_samples(F.res_x, F.res_y, F.local_rows, F.row0, F.band_index, F.band_count, F.band_rows,
+                                     F.spp);
     const int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
@@ -550,7 +625,16 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F, bool count_t
         hipLaunchKernelGGL((render_kernel<false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+    if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
+        const int waves = blocks * kMkWaves;
+        hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
+                           (const uint4 *)F.wave_counts, waves, F.primary_total, F.counters);
+    }
     return hipGetLastError();
+}
+
+int render_mega_waves(const FrameDev &F) {
+    return F.num_tiles <= 0 ? 0 : F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles;
 }
 
 // Longest-first dispatch for the next frame: tiles sorted by the cost key this

@@ -400,9 +400,17 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
     return v;
 }
 
+// The wave's sharded counter slot (rt_stats order, rt_device.h).
+__device__ __forceinline__ unsigned long long *counter_slot(unsigned long long *counters) {
+    return counters + (size_t)(blockIdx.x % rtd::kCounterSlots) * rtd::kCounterWords;
+}
+
 template <bool COUNT>
 __device__ __forceinline__ void flush_counts(const Counts &c, unsigned long long *counters) {
-    unsigned long long *ctr = counters + (size_t)(blockIdx.x % rtd::kCounterSlots) * rtd::kCounterWords;
+    // a wave whose rays were all counted already (or none): no reductions, no
+    // atomics — a wave's slot is held until its atomics are acknowledged
+    if (!COUNT && __ballot((c.primary | c.shadow | c.reflection | c.moot) != 0) == 0) return;
+    unsigned long long *ctr = counter_slot(counters);
     const unsigned p = wave_sum(c.primary), s = wave_sum(c.shadow), r = wave_sum(c.reflection),
                    m = wave_sum(c.moot);
     unsigned b = 0, t = 0, q = 0, h = 0, g = 0;
