@@ -205,8 +205,9 @@ struct FrameDev {
     // exact rays: each of them misses the exact Scene.AABB gate (Scene.cs:54),
     // so Shade returns the background (RayTracingSetup.cs:310-311).
     unsigned long long primary_total;  // render_kernel (non-counting): camera samples of this launch, added once
-    uint4 *wave_counts;      // render_kernel (non-counting): per-wave {shadow, reflection, moot} tallies, one
-                             // uint4 per wave of the launch, reduced after it; null: per-wave atomics
+    uint4 *wave_counts;      // render_kernel (non-counting): per-wave {shadow, reflection, moot, tag} tallies,
+                             // one uint4 per wave of the launch, reduced after it; null: per-wave atomics
+    unsigned count_tag;      // this launch's tag in wave_counts (unique per context launch, never 0)
     int sky_test;            // 1: on (camera outside the padded box, all inputs finite)
     float sky_tlc[3];        // top_left - cam_pos
     float sky_hx, sky_vy;    // HorizontalLength / res_x, VerticalLength / res_y

@@ -267,8 +267,9 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
 // one of the four (pshift 4: 16 lanes) or sixteen (pshift 2: 4 lanes) waves
 // an expensive tile is split into.
+// Returns true when the tile was answered by the sky test (no exact rays).
 template <bool COUNT, bool DEEP, bool Q4>
-__device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
+__device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
                                             SegClock &sg) {
     int px, ly, gy, s;
@@ -305,7 +306,7 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
     const bool active2 =
         rts::slot_pixel<Q4>(F, tile2, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
 #ifdef RT_EXP_SKYNOSTORE
-    if (sky) return;  // measurement only: what a sky wave's pixel store costs
+    if (sky) return sky;  // measurement only: what a sky wave's pixel store costs
 #endif
     if (active2 && s == 0) {
         f3 v = sum;
@@ -315,7 +316,9 @@ __device__ __forceinline__ void render_tile(const SceneDev &S, const FrameDev &F
             v = v / (float)F.spp;
         rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
     }
+    return sky;
 }
+
 
 // SPLIT: the variant launched when a frame splits tiles (a separate instance, so
 // the common kernel's code and register allocation stay as they are); DEEP:
@@ -340,26 +343,30 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     // waves of one pixel's 4 samples each, the next split_tiles as four
     // quarter-waves each (16 lanes: a smaller, more coherent packet, a
     // shorter wave)
-    int tile, part = -1, pshift = 4;
+    int idx, part = -1, pshift = 4;
     if (SPLIT && wid < 16 * split16) {
-        tile = rtt::cload(F.tile_order + (wid >> 4));  // scalar load: tile math stays SALU
+        idx = wid >> 4;
         part = wid & 15;
         pshift = 2;
     } else if (SPLIT && wid < 16 * split16 + 4 * split) {
         const int w1 = wid - 16 * split16;
-        tile = rtt::cload(F.tile_order + split16 + (w1 >> 2));
+        idx = split16 + (w1 >> 2);
         part = w1 & 3;
     } else {
-        const int w2 = wid - 15 * split16 - 3 * split;
-        tile = F.tile_order ? rtt::cload(F.tile_order + w2) : w2;
+        idx = wid - 15 * split16 - 3 * split;
     }
+    const int tile = F.tile_order ? rtt::cload(F.tile_order + idx) : idx;  // scalar load: tile math stays SALU
     // the launch's camera samples (one per active lane of every tile, computed
     // by the host: rt_device.h active_samples), counted once per launch
     if (!COUNT && !F.wave_counts && wid == 0 && lane == 0) atomicAdd(rtt::counter_slot(F.counters), F.primary_total);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    const bool sky = render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    if (F.tile_cost && lane == 0 && part <= 0) {
+        // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
+        F.tile_cost[tile] = sky ? 0u : max(1u, tile_cost_key(__builtin_amdgcn_s_memtime() - t0, part, pshift));
+    }
 #ifdef RT_SEG_PROFILE
     if (!COUNT) {
         const unsigned long long ts1 = __builtin_amdgcn_s_memtime();
@@ -389,9 +396,6 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
         }
     }
 #endif
-    if (F.tile_cost && lane == 0 && part <= 0) {
-        F.tile_cost[tile] = tile_cost_key(__builtin_amdgcn_s_memtime() - t0, part, pshift);
-    }
 #ifndef RT_EXP_NOFLUSH
     if (!COUNT && F.wave_counts) {
         // the wave's tallies by a plain store (reduced by wave_counts_kernel
@@ -403,7 +407,7 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
             rf = rtt::wave_sum(cnt.reflection);
             mo = rtt::wave_sum(cnt.moot);
         }
-        if (lane == 0) F.wave_counts[wid] = make_uint4(sh, rf, mo, 0u);
+        if (lane == 0) F.wave_counts[wid] = make_uint4(sh, rf, mo, F.count_tag);
     } else {
         rtt::flush_counts<COUNT>(cnt, F.counters);
     }
@@ -413,11 +417,15 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
 // Per-wave tallies of a render_kernel launch (F.wave_counts) -> the frame's
 // sharded counters: shadow, reflection and moot rays, plus the launch's
 // camera samples (F.primary_total) once.
-__global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n, unsigned long long primary_total,
+// Only entries carrying this launch's tag count (a stale entry of another
+// launch never does).
+__global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n, unsigned tag,
+                                                         unsigned long long primary_total,
                                                          unsigned long long *counters) {
     unsigned long long sh = 0, rf = 0, mo = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const uint4 v = wc[i];
+        if (v.w != tag) continue;
         sh += v.x;
         rf += v.y;
         mo += v.z;
@@ -628,7 +636,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = blocks * kMkWaves;
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
-                           (const uint4 *)F.wave_counts, waves, F.primary_total, F.counters);
+                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
     }
     return hipGetLastError();
 }
