@@ -21,16 +21,25 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(dirs):
-    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch]
+    """kernel -> counter -> [per-dispatch values], over the dispatches of the
+    kernel's largest grid only: the workload's launches, not the tiny warm-up
+    frames a context renders at its first rt_set_scene (same kernel names)."""
+    vals = defaultdict(lambda: defaultdict(list))
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             per = defaultdict(lambda: defaultdict(float))
-            names = {}
+            names, grids = {}, {}
             for row in csv.DictReader(open(f)):
                 did = row.get("Dispatch_Id") or row.get("Correlation_Id")
                 names[did] = row["Kernel_Name"]
+                grids[did] = int(float(row.get("Grid_Size") or 0))
                 per[did][row["Counter_Name"]] += float(row["Counter_Value"])
+            biggest = defaultdict(int)
+            for did, g in grids.items():
+                biggest[names[did]] = max(biggest[names[did]], g)
             for did, cs in per.items():
+                if grids[did] != biggest[names[did]]:
+                    continue
                 for c, v in cs.items():
                     vals[names[did]][c].append(v)
     return vals

@@ -298,13 +298,15 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
             color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg);
         }
     }
-    const f3 sum = rts::sample_sum(color, lane, F.spp);
-    // the slot -> pixel mapping is recomputed from the (scalar) tile index
+    const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
+    // the slot -> pixel mapping is recomputed from the (scalar) tile index and
+    // the lane id (v_mbcnt, opaque to the compiler so it is not kept live)
     // rather than kept live across the trace, where it would be spilled
     int tile2 = __builtin_amdgcn_readfirstlane(tile);
     asm volatile("" : "+s"(tile2));
+    const int lane2 = rtt::lane_id();
     const bool active2 =
-        rts::slot_pixel<Q4>(F, tile2, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
+        rts::slot_pixel<Q4>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
 #ifdef RT_EXP_SKYNOSTORE
     if (sky) return sky;  // measurement only: what a sky wave's pixel store costs
 #endif
@@ -329,9 +331,10 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
     __shared__ int wstack_mem[kMkWaves * rtp::kWaveStack];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    // wave-uniform (an SGPR; with one-wave workgroups simply the block index)
+    const int wave = kMkWaves == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize, ovf};  // + lane per query (traverse)
     int *const wstack = wstack_mem + wave * rtp::kWaveStack;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x * kMkWaves + wave;
@@ -355,7 +358,11 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     } else {
         idx = wid - 15 * split16 - 3 * split;
     }
-    const int tile = F.tile_order ? rtt::cload(F.tile_order + idx) : idx;  // scalar load: tile math stays SALU
+    // the tile index is wave-uniform and kept in an SGPR: the slot -> pixel
+    // integer math runs on the scalar unit and nothing of it is spilled
+    int tile = idx;
+    if (F.tile_order) tile = rtt::cload(F.tile_order + idx);
+    tile = __builtin_amdgcn_readfirstlane(tile);
     // the launch's camera samples (one per active lane of every tile, computed
     // by the host: rt_device.h active_samples), counted once per launch
     if (!COUNT && !F.wave_counts && wid == 0 && lane == 0) atomicAdd(rtt::counter_slot(F.counters), F.primary_total);
@@ -363,7 +370,8 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
     const bool sky = render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
-    if (F.tile_cost && lane == 0 && part <= 0) {
+    const int lane_e = rtt::lane_id();  // not kept live across the trace
+    if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
         F.tile_cost[tile] = sky ? 0u : max(1u, tile_cost_key(__builtin_amdgcn_s_memtime() - t0, part, pshift));
     }
@@ -407,7 +415,7 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
             rf = rtt::wave_sum(cnt.reflection);
             mo = rtt::wave_sum(cnt.moot);
         }
-        if (lane == 0) F.wave_counts[wid] = make_uint4(sh, rf, mo, F.count_tag);
+        if (lane_e == 0) F.wave_counts[wid] = make_uint4(sh, rf, mo, F.count_tag);
     } else {
         rtt::flush_counts<COUNT>(cnt, F.counters);
     }
@@ -467,7 +475,7 @@ __global__ __launch_bounds__(kBlockThreads) void render_packet_kernel(SceneDev S
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize, ovf};  // + lane per query (traverse)
     int *wstack = wstack_mem + wave * rtp::kWaveStack;
     const int tile = blockIdx.x * kWavesPerBlock + wave;
     if (tile >= F.num_tiles) return;  // wave-uniform
@@ -558,10 +566,9 @@ __global__ __launch_bounds__(kBlockThreads) void render_packet_kernel(SceneDev S
 
 __global__ __launch_bounds__(kBlockThreads) void intersect_kernel(SceneDev S, const float *rays, int n, int4 *out) {
     __shared__ int stack_mem[kWavesPerBlock * kStackSize * kWaveSize];
-    const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize + lane, ovf};
+    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize, ovf};  // + lane per query (traverse)
     const int i = blockIdx.x * kBlockThreads + threadIdx.x;
     if (i >= n) return;
     const float *rr = rays + (size_t)i * 6;

@@ -375,16 +375,27 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
 
 #undef RT_CSWAP
 
-// Whole query in one call (megakernel / batch-intersect path).
+// The lane id, through an opaque v_mbcnt pair: the compiler cannot keep a
+// copy of it (or of anything derived from it) live across a long trace, where
+// it would be spilled — it is recomputed where used (2 VALU).
+__device__ __forceinline__ int lane_id() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+// Whole query in one call (megakernel / batch-intersect path).  `wave_st.lds`
+// is the wave's LDS stack base; the lane's column is added here, per query.
 template <bool ANY, bool COUNT, bool MESH_ONLY = false>
 __device__ __forceinline__ bool traverse(const rtd::SceneDev &S, const RayCtx &r, float tlimit, float d2,
-                                         float &best_t, int &best_rank, const Stack &st, Counts &cnt) {
+                                         float &best_t, int &best_rank, const Stack &wave_st, Counts &cnt) {
     Trav t;
     if (!trav_begin<ANY, COUNT>(S, r, tlimit, t, cnt)) {
         best_t = FLT_MAX;
         best_rank = -1;
         return false;
     }
+    const Stack st{wave_st.lds + lane_id(), wave_st.ovf};
     while (!trav_step<ANY, COUNT, MESH_ONLY>(S, r, t, d2, st, cnt)) {
     }
     best_t = t.best_t;
