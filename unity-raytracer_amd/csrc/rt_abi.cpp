@@ -417,6 +417,7 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.res_y = plane->resolution_y;
     F.spp = n * n;
     F.spp_n = n;
+    F.inv_spp = 1.0f / (float)F.spp;
     F.max_bounces = prm->max_reflection_bounces;
     F.band_index = prm->band_index;
     F.band_count = band_count;
@@ -698,7 +699,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // render_kernel's ray tallies: one plain store per wave into this slot's
     // buffer, reduced after the launch on the same stream (an atomic per wave
     // holds the wave's slot for its round trip: C2 -13 %, C3 -4 %)
-    if (!count && !(ctx->S.bvh4 && F.spp >= 16)) {
+    if (!count) {  // render_kernel and render_levels_kernel
         const size_t bytes = (size_t)rtk::render_mega_waves(F) * sizeof(uint4);
         if (bytes > ls->wave_counts.cap) {  // a new buffer carries no launch's tag
             HIP_OR_FAIL(ctx, ensure(ctx, ls->wave_counts, bytes));

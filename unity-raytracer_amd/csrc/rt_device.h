@@ -208,6 +208,7 @@ struct FrameDev {
     uint4 *wave_counts;      // render_kernel (non-counting): per-wave {shadow, reflection, moot, tag} tallies,
                              // one uint4 per wave of the launch, reduced after it; null: per-wave atomics
     unsigned count_tag;      // this launch's tag in wave_counts (unique per context launch, never 0)
+    float inv_spp;           // 1 / spp, exact when spp is a power of two (x * inv_spp == x / spp then)
     int sky_test;            // 1: on (camera outside the padded box, all inputs finite)
     float sky_tlc[3];        // top_left - cam_pos
     float sky_hx, sky_vy;    // HorizontalLength / res_x, VerticalLength / res_y

@@ -315,7 +315,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
         if (Q4)
             v = v * 0.25f;  // == v / 4: the same real number, rounded once
         else if (F.spp > 1)
-            v = v / (float)F.spp;
+            v = (F.spp & (F.spp - 1)) == 0 ? v * F.inv_spp : v / (float)F.spp;  // likewise for 2^k
         rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
     }
     return sky;
@@ -634,8 +634,14 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         hipLaunchKernelGGL((render_kernel<false, true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (F.split_tiles > 0 || F.split16_tiles > 0)
         hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    else if (S.bvh4 && F.spp >= kLevelsMinSpp)
-        return launch_render_levels(S, F, stream);
+    else if (S.bvh4 && F.spp >= kLevelsMinSpp) {
+        const hipError_t e = launch_render_levels(S, F, stream);
+        if (e != hipSuccess || !F.wave_counts) return e;
+        const int waves = F.num_tiles;  // one wave per tile, no splits
+        hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
+                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
+        return hipGetLastError();
+    }
     else if (q4)
         hipLaunchKernelGGL((render_kernel<false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else

@@ -22,24 +22,34 @@ using rtt::Counts;
 
 namespace {
 
-constexpr int kLvMinWaves = 7;
+// Waves per SIMD the register budget must allow: 6 (80 VGPRs, fewer spills in
+// the level loop) for up to 16 spp, 7 (72 VGPRs) above.  Measured (round 3,
+// interleaved A/B): C4 (16 spp, depth 8) 6 waves -5 % single frame / -8 %
+// frames in flight against 7; C5 (64 spp, depth 16) 6 waves +2 %, 5 waves
+// +6 %.
+constexpr int kLvWavesLowSpp = 6;
+constexpr int kLvWavesHighSpp = 7;
 
 // Level-synchronous all-packet megakernel (the default non-counting path on
 // a 4-wide BVH): one wave = one tile of 64 samples; the Whitted chain
 // advances level by level for the whole wave, and every level's rays — the
 // camera rays, the mirror rays of the lanes still bouncing, and each level's
 // shadow rays — are traced as wave packets (packet.h).  Without a per-lane
-// traversal the kernel needs no LDS lane stack and ~80 VGPRs (6 waves/SIMD,
-// no spills); the mirror fold (c + km*(...), evaluated back to front as the
+// traversal the kernel needs no LDS lane stack and 72-80 VGPRs (7 or 6
+// waves/SIMD, kLvWaves*); the mirror fold (c + km*(...), evaluated back to front as the
 // recursion rounds) lives in scratch and is touched only by mirror lanes.
 // Same arithmetic per sample as render_kernel.
-__global__ __launch_bounds__(kWaveSize, kLvMinWaves) void render_levels_kernel(SceneDev S, FrameDev F) {
+template <int MIN_WAVES>
+__global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
     const int lane = threadIdx.x & 63;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x;
     if (wid >= F.num_tiles) return;  // wave-uniform
-    const int tile = F.tile_order ? rtt::cload(F.tile_order + wid) : wid;
+    // the tile index in an SGPR (scalar slot -> pixel math, nothing spilled)
+    int tile = wid;
+    if (F.tile_order) tile = rtt::cload(F.tile_order + wid);
+    tile = __builtin_amdgcn_readfirstlane(tile);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
@@ -52,7 +62,7 @@ __global__ __launch_bounds__(kWaveSize, kLvMinWaves) void render_levels_kernel(S
         alive = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
         if (alive) {
             rts::primary_ray(F, px, gy, s, o, d);
-            cnt.primary = 1;
+            if (!F.wave_counts) cnt.primary = 1;  // otherwise F.primary_total, once per launch
         }
     }
     for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
@@ -105,23 +115,35 @@ __global__ __launch_bounds__(kWaveSize, kLvMinWaves) void render_levels_kernel(S
     }
     for (int k = depth - 1; k >= 0; --k)
         term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
-    const f3 sum = rts::sample_sum(term, lane, F.spp);
+    // lane ids recomputed (rtt::lane_id), not kept live across the levels
+    const int lane2 = rtt::lane_id();
+    const f3 sum = rts::sample_sum(term, lane2, F.spp);
     {
         int tile2 = __builtin_amdgcn_readfirstlane(tile);
         asm volatile("" : "+s"(tile2));
         int px, ly, gy, s;
-        if (rts::slot_pixel(F, tile2, lane, px, ly, gy, s) && s == 0) {
+        if (rts::slot_pixel(F, tile2, lane2, px, ly, gy, s) && s == 0) {
             f3 v = sum;
-            if (F.spp > 1) v = v / (float)F.spp;
+            if (F.spp > 1) v = (F.spp & (F.spp - 1)) == 0 ? v * F.inv_spp : v / (float)F.spp;
             rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
         }
     }
-    if (F.tile_cost && lane == 0) {
+    if (F.tile_cost && lane2 == 0) {
         const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
         const unsigned e = c ? 31u - __clz(c) : 0u;
         F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
     }
-    rtt::flush_counts<false>(cnt, F.counters);
+    if (F.wave_counts) {  // plain store, reduced after the launch (trace.hip wave_counts_kernel)
+        unsigned sh = 0, rf = 0, mo = 0;
+        if (__ballot((cnt.shadow | cnt.reflection | cnt.moot) != 0) != 0) {
+            sh = rtt::wave_sum(cnt.shadow);
+            rf = rtt::wave_sum(cnt.reflection);
+            mo = rtt::wave_sum(cnt.moot);
+        }
+        if (lane2 == 0) F.wave_counts[wid] = make_uint4(sh, rf, mo, F.count_tag);
+    } else {
+        rtt::flush_counts<false>(cnt, F.counters);
+    }
 }
 
 }  // namespace
@@ -130,7 +152,11 @@ namespace rtk {
 
 hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
-    hipLaunchKernelGGL(render_levels_kernel, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S, F);
+    if (F.spp <= 16)
+        hipLaunchKernelGGL(render_levels_kernel<kLvWavesLowSpp>, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S, F);
+    else
+        hipLaunchKernelGGL(render_levels_kernel<kLvWavesHighSpp>, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S,
+                           F);
     return hipGetLastError();
 }
 
