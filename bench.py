@@ -172,13 +172,15 @@ def host_facts():
     return {"nproc": os.cpu_count() or 1, "affinity_cpus": affinity, "cpu_model": model}
 
 
-def cpu_baseline(rt, fr, budget_s):
+def cpu_baseline(rt, fr, budget_s, ctx):
     """The C oracle (brute force, the reference's algorithm) on seeded random
     pixels of the same frame: 1 thread (the reference is single-threaded
     Mono) for budget_s, then OpenMP over every host core this job is given
     (the affinity mask, capped by OMP_NUM_THREADS: the GPU box grants a
     one-GPU job 16 cores of a larger machine) for budget_s / 3, then the same
-    threads with a CPU BVH for budget_s / 3.  Mrays/s with the same ray
+    threads with a CPU BVH for budget_s / 3, then with the GPU's own tree
+    (bvh_same_tree, rt_export_bvh) for budget_s / 3; plus whole C1 and C2
+    frames (median of 5, 1 thread and all threads).  Mrays/s with the same ray
     accounting as the GPU line."""
     orc = _rt_pkg.load_oracle()
     rng = np.random.default_rng(20250101)
@@ -216,6 +218,35 @@ def cpu_baseline(rt, fr, budget_s):
         brays += c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
         bpix += len(idx)
     bvh.close()
+    # the GPU's own tree (rt_export_bvh) traversed on the CPU, same threads
+    nodes, tris, sphs = ctx.export_bvh()
+    b4 = orc.Bvh4Scene(fr, nodes, tris, sphs)
+    srays, ssecs, spix = 0, 0.0, 0
+    while ssecs < budget_s / 3:
+        idx = rng.integers(0, total, 64 * threads).astype(np.int32)
+        t0 = time.perf_counter()
+        _, c = b4.render_pixels(idx, threads=threads)
+        ssecs += time.perf_counter() - t0
+        srays += c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
+        spix += len(idx)
+    b4.close()
+    # whole frames of the small configs (C1 and C2 in full), the
+    # reference's brute force at 1 thread and at the job's threads, median of 5
+    full = {}
+    for name, reps in (("C1", 5), ("C2", 5)):
+        ff = rt.make(name)
+        for nt in (1, threads):
+            ts, rays_f = [], 0
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                _, c = orc.render(ff, threads=nt)
+                ts.append(time.perf_counter() - t0)
+                rays_f = c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
+            med = float(np.median(ts))
+            full[f"{name.lower()}_full" + ("" if nt == 1 else "_all_cores")] = {
+                "mrays_per_s": rays_f / med / 1e6, "ms_per_frame": med * 1e3, "rays_per_frame": rays_f,
+                "threads": nt, "runs": reps, "frame": f"{ff.plane.ResolutionX}x{ff.plane.ResolutionY}, "
+                                                    f"{ff.spp} spp, depth {ff.max_bounces}"}
     return {
         "value": rays / secs / 1e6,
         "unit": "Mrays/s",
@@ -231,6 +262,11 @@ def cpu_baseline(rt, fr, budget_s):
         "bvh_all_cores_sample": f"{bpix} seeded random pixels, {brays} rays in {bsecs:.1f} s, the oracle with a "
                                 f"CPU BVH (median split, leaves <= 4; same answers as the scan), "
                                 f"{threads} threads",
+        "bvh_same_tree": {"mrays_per_s": srays / ssecs / 1e6, "threads": threads,
+                          "sample": f"{spix} seeded random pixels, {srays} rays in {ssecs:.1f} s: the GPU's own "
+                                    f"4-wide SAH tree (rt_export_bvh) traversed per ray on the CPU like "
+                                    f"csrc/traverse.h (near-first closest hits, any-hit shadow rays)"},
+        **full,
         **facts,
     }
 
@@ -654,7 +690,7 @@ def main():
             "roofline": roofline(pmc, pmc_state, kname, avg_kernel_s, logical),
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(rt, fr, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(rt, fr, args.cpu_seconds, ctx)
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist_on:

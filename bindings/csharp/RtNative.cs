@@ -121,6 +121,12 @@ namespace RayTracer.Native
     }
 
     [StructLayout(LayoutKind.Sequential)]
+    public struct RtBvhExportInfo
+    {
+        public int Nodes, TriangleRecords, SphereRecords, Reserved;
+    }
+
+    [StructLayout(LayoutKind.Sequential)]
     public struct RtRay { public float3 Origin, Direction; }
 
     [StructLayout(LayoutKind.Sequential)]
@@ -150,6 +156,9 @@ namespace RayTracer.Native
         [DllImport(Lib)] public static extern int rt_set_scene(IntPtr ctx, ref RtSceneDesc scene);
         [DllImport(Lib)] public static extern int rt_set_scene_ex(IntPtr ctx, ref RtSceneDesc scene, int build);
         [DllImport(Lib)] public static extern int rt_get_scene_info(IntPtr ctx, out RtSceneInfo info);
+        // inspection: the 4-wide BVH as it lies in HBM (null arrays: counts only)
+        [DllImport(Lib)] public static extern int rt_export_bvh(IntPtr ctx, [Out] byte[] nodes, [Out] byte[] triangleRecords,
+                                                               [Out] byte[] sphereRecords, out RtBvhExportInfo info);
         [DllImport(Lib)] public static extern int rt_set_scene_source(IntPtr ctx, ref RtSceneDesc baseScene,
                                                                      [In] RtMeshSource[] meshes, int meshCount);
         [DllImport(Lib)] public static extern int rt_update_mesh_transforms(IntPtr ctx, [In] RtMatrix[] localToWorld,

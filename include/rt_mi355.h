@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum rt_status {
@@ -290,6 +290,24 @@ typedef struct rt_scene_info {
 } rt_scene_info;
 
 int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info);
+
+/* Inspection: the scene's 4-wide BVH exactly as it lies in HBM — 128-B nodes
+ * (child boxes plane by plane, child refs: >= 0 node, < 0 inline leaf
+ * ~(first | (count-1) << 27 | kind << 29)), 48-B triangle records in leaf
+ * order (v0, v1 - v0, v2 - v0, reference rank, mesh gate; one sentinel record
+ * last), 32-B sphere records (center, r^2, rank) — copied into caller
+ * buffers.  For tools and the CPU baseline that traverses the very tree the
+ * GPU does (bench.py cpu_baseline).  Null buffers: only *info is filled.
+ * RT_E_STATE without a scene or for a 2-wide (RT_BUILD_LBVH_GPU_BVH2) tree. */
+typedef struct rt_bvh_export_info {
+    int32_t nodes;           /* 128-B node records   */
+    int32_t triangle_records;/* 48-B triangle records (incl. the sentinel) */
+    int32_t sphere_records;  /* 32-B sphere records  */
+    int32_t reserved;
+} rt_bvh_export_info;
+
+int rt_export_bvh(const rt_ctx *ctx, void *nodes, void *triangle_records, void *sphere_records,
+                  rt_bvh_export_info *info);
 
 /* One mesh as the reference holds it before extraction: SceneMesh's
  * MeshFilter.sharedMesh (vertices, index buffer) and Transform

@@ -66,6 +66,11 @@ def lib():
         L.orc_bvh_free.argtypes = [P]
         L.orc_bvh_free.restype = None
         L.orc_render_pixels_bvh.argtypes = [P, P, P, P, P, P, C.c_int32, P, P, C.c_int32]
+        L.orc_bvh4_create.argtypes = [P, P, C.c_int32, P, C.c_int32, P, C.c_int32]
+        L.orc_bvh4_create.restype = P
+        L.orc_bvh4_free.argtypes = [P]
+        L.orc_bvh4_free.restype = None
+        L.orc_render_pixels_bvh4.argtypes = [P, P, P, P, P, P, C.c_int32, P, P, C.c_int32]
         _lib = L
     return _lib
 
@@ -178,6 +183,43 @@ class BvhScene:
     def close(self):
         if self.h:
             lib().orc_bvh_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class Bvh4Scene:
+    """A scene with the GPU's own 4-wide BVH (the byte records rt_export_bvh
+    returns: 128-B nodes, 48-B triangle and 32-B sphere records), traversed on
+    the CPU per ray like csrc/traverse.h (CPU-baseline only: the same tree as
+    the GPU, so the algorithmic vs hardware split is like for like)."""
+
+    def __init__(self, fr, nodes, tris, sphs):
+        self.fr = fr
+        self.desc = fr.scene.to_desc()
+        self.keep = [np.ascontiguousarray(a, np.uint8) for a in (nodes, tris, sphs)]
+        n, t, s = self.keep
+        self.h = lib().orc_bvh4_create(C.cast(self.desc.ref(), C.c_void_p), _p(n), len(n) // 128, _p(t),
+                                       len(t) // 48, _p(s), len(s) // 32)
+        if not self.h:
+            raise RuntimeError("oracle BVH4 create failed")
+
+    def render_pixels(self, pixel_indices, threads: int = 0, spp=None):
+        cam, pl, prm = _frame_structs(self.fr, spp)
+        idx = np.ascontiguousarray(pixel_indices, np.int32)
+        out = np.zeros((len(idx), 4), np.float32)
+        cnt = orc_counts()
+        st = lib().orc_render_pixels_bvh4(self.h, C.cast(self.desc.ref(), C.c_void_p), C.byref(cam), C.byref(pl),
+                                          C.byref(prm), _p(idx), len(idx), _p(out), C.byref(cnt),
+                                          threads or default_threads())
+        if st != 0:
+            raise RuntimeError(f"oracle render failed: {st}")
+        return out, cnt.as_dict()
+
+    def close(self):
+        if self.h:
+            lib().orc_bvh4_free(self.h)
             self.h = None
 
     def __del__(self):

@@ -415,15 +415,196 @@ static rt_hit bvh_intersect(const orc_bvh *B, const rt_scene_desc *sc, const rt_
     return hit;
 }
 
+/* ------------------------------------------------------------------------
+ * The GPU's own 4-wide BVH (rt_export_bvh: the records exactly as they lie
+ * in HBM, unity-raytracer_amd/csrc/rt_device.h) traversed on the CPU — the
+ * CPU-baseline leg that runs the very tree the GPU runs, so the split between
+ * the algorithm's speed-up and the hardware's is like for like.  Per ray, as
+ * the GPU's per-lane traversal (csrc/traverse.h): the exact scene gate, then
+ * near-first closest hit over the padded node boxes (ties to the lowest
+ * reference rank), the exact Mesh.AABB gate per leaf (Scene.cs:67), and
+ * shadow rays as any-hit queries with the predicate t*t < d2.  Same answers as
+ * the brute-force scan (the GPU parity tests hold that for this tree).
+ * --------------------------------------------------------------------- */
+typedef struct { float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4]; int32_t child[4], pad[4]; } orc_node4;
+typedef struct { float p0[4], p1[4], p2[4]; } orc_trirec;  /* v0 e1.x | e1.yz e2.xy | e2.z rank gate - */
+typedef struct { float cr[4]; int32_t misc[4]; } orc_sphrec;  /* center r2 | rank gate - - */
+
+typedef struct orc_bvh4 {
+    orc_node4 *nodes;
+    orc_trirec *tris;
+    orc_sphrec *sphs;
+    int nnodes, ntris, nsphs, mt, ns, mesh_count;
+    int *mesh_of; /* rank -> mesh (mesh triangles) */
+} orc_bvh4;
+
+static inline int rbits(float f) { int i; memcpy(&i, &f, 4); return i; }
+
+void *orc_bvh4_create(const rt_scene_desc *sc, const void *nodes, int32_t nnodes, const void *tris, int32_t ntris,
+                      const void *sphs, int32_t nsphs) {
+    orc_bvh4 *B = (orc_bvh4 *)calloc(1, sizeof *B);
+    if (!B) return NULL;
+    B->nnodes = nnodes; B->ntris = ntris; B->nsphs = nsphs;
+    B->mt = sc->mesh_triangle_total; B->ns = sc->sphere_count; B->mesh_count = sc->mesh_count;
+    B->nodes = (orc_node4 *)malloc(sizeof(orc_node4) * (size_t)(nnodes > 0 ? nnodes : 1));
+    B->tris = (orc_trirec *)malloc(sizeof(orc_trirec) * (size_t)(ntris > 0 ? ntris : 1));
+    B->sphs = (orc_sphrec *)malloc(sizeof(orc_sphrec) * (size_t)(nsphs > 0 ? nsphs : 1));
+    B->mesh_of = (int *)malloc(sizeof(int) * (size_t)(B->mt > 0 ? B->mt : 1));
+    if (nnodes) memcpy(B->nodes, nodes, sizeof(orc_node4) * (size_t)nnodes);
+    if (ntris) memcpy(B->tris, tris, sizeof(orc_trirec) * (size_t)ntris);
+    if (nsphs) memcpy(B->sphs, sphs, sizeof(orc_sphrec) * (size_t)nsphs);
+    for (int m = 0; m < sc->mesh_count; ++m)
+        for (int i = 0; i < sc->meshes[m].triangle_count; ++i) B->mesh_of[sc->meshes[m].first_triangle + i] = m;
+    return B;
+}
+
+void orc_bvh4_free(void *h) {
+    orc_bvh4 *B = (orc_bvh4 *)h;
+    if (!B) return;
+    free(B->nodes); free(B->tris); free(B->sphs); free(B->mesh_of);
+    free(B);
+}
+
+/* One query.  any: shadow ray, true when some primitive has t*t < d2 (node
+ * culling at tlimit); otherwise the closest hit (best, best_rank). */
+static int bvh4_query(const orc_bvh4 *B, const rt_scene_desc *sc, const rt_aabb *scene_box, const rt_ray *ray,
+                      int any, float tlimit, float d2, float *best_out, int *rank_out, orc_tests *ct) {
+    *best_out = FLT_MAX;
+    *rank_out = -1;
+    ct->box++;
+    if (B->nnodes == 0 || !orc_ray_aabb(ray, scene_box)) return 0; /* Scene.cs:54 */
+    if (t_gate_n < B->mesh_count) {
+        free(t_gate);
+        t_gate = (unsigned long long *)calloc((size_t)B->mesh_count, sizeof *t_gate);
+        t_gate_n = B->mesh_count;
+    }
+    const unsigned long long stamp = ++t_stamp;
+    const float o[3] = {ray->origin.x, ray->origin.y, ray->origin.z};
+    const float inv[3] = {1.0f / ray->direction.x, 1.0f / ray->direction.y, 1.0f / ray->direction.z};
+    float best = FLT_MAX, cull = any ? tlimit : FLT_MAX;
+    int best_rank = 0x7fffffff;
+    int stack[256], sp = 0, ref = 0;
+    for (;;) {
+        if (ref >= 0) {
+            const orc_node4 *nd = &B->nodes[ref];
+            const float *lo[3] = {nd->lox, nd->loy, nd->loz}, *hi[3] = {nd->hix, nd->hiy, nd->hiz};
+            float key[4];
+            int ch[4], nh = 0;
+            for (int c = 0; c < 4; ++c) {
+                float tn = 0.0f, tf = cull;
+                for (int a = 0; a < 3; ++a) { /* padded box; NaN operands ignored */
+                    const float t1 = (lo[a][c] - o[a]) * inv[a], t2 = (hi[a][c] - o[a]) * inv[a];
+                    tn = fmaxf(tn, fminf(t1, t2));
+                    tf = fminf(tf, fmaxf(t1, t2));
+                }
+                ct->box++;
+                if (tn <= tf) {
+                    /* insertion by entry distance: near first (any-hit: slot order) */
+                    int k = nh++;
+                    while (!any && k > 0 && key[k - 1] > tn) { key[k] = key[k - 1]; ch[k] = ch[k - 1]; --k; }
+                    key[k] = tn;
+                    ch[k] = nd->child[c];
+                }
+            }
+            if (nh == 0) goto pop;
+            for (int k = nh - 1; k >= 1; --k) stack[sp++] = ch[k];
+            ref = ch[0];
+            continue;
+        } else {
+            const int v = ~ref, first = v & ((1 << 27) - 1), count = ((v >> 27) & 3) + 1, kind = (v >> 29) & 1;
+            for (int i = first; i < first + count; ++i) {
+                float t;
+                int ok, rank;
+                if (kind == 0) {
+                    const orc_trirec *r = &B->tris[i];
+                    const int gate = rbits(r->p2[2]);
+                    rank = rbits(r->p2[1]);
+                    if (gate >= 0) {
+                        unsigned long long g = t_gate[gate];
+                        if ((g >> 1) != stamp) { /* Mesh.AABB gate, Scene.cs:67, once per ray and mesh */
+                            ct->box++;
+                            g = (stamp << 1) | (unsigned long long)(orc_ray_aabb(ray, &sc->meshes[gate].aabb) != 0);
+                            t_gate[gate] = g;
+                        }
+                        if (!(g & 1)) continue;
+                    }
+                    ct->tri++;
+                    /* RMath.RayTriangleIntersection :29-73 on the stored edges (v1 - v0, v2 - v0) */
+                    const f3 d = ray->direction, v0 = V(r->p0[0], r->p0[1], r->p0[2]);
+                    const f3 e1 = V(r->p0[3], r->p1[0], r->p1[1]), e2 = V(r->p1[2], r->p1[3], r->p2[0]);
+                    const f3 h = cross(d, e2);
+                    const float a = dot(e1, h);
+                    if (a > -RMATH_EPSILON && a < RMATH_EPSILON) continue;
+                    const float f = 1.0f / a;
+                    const f3 sv = sub(ray->origin, v0);
+                    const float u = f * dot(sv, h);
+                    if (u < 0.0f || u > 1.0f) continue;
+                    const f3 q = cross(sv, e1);
+                    const float vv = f * dot(d, q);
+                    if (vv < 0.0f || u + vv > 1.0f) continue;
+                    t = f * dot(e2, q);
+                    ok = t > RMATH_EPSILON;
+                } else {
+                    const orc_sphrec *r = &B->sphs[i];
+                    rt_sphere sp2;
+                    sp2.center = V(r->cr[0], r->cr[1], r->cr[2]);
+                    sp2.radius_squared = r->cr[3];
+                    rank = r->misc[0];
+                    ct->sph++;
+                    ok = orc_ray_sphere(ray, &sp2, &t);
+                }
+                if (!ok) continue;
+                if (any) {
+                    if (t * t < d2) { *rank_out = 1; return 1; }
+                } else if (t < best || (t == best && rank < best_rank)) {
+                    best = t;
+                    best_rank = rank;
+                    cull = t;
+                }
+            }
+        }
+    pop:
+        if (sp == 0) break;
+        ref = stack[--sp];
+    }
+    if (!any && best_rank != 0x7fffffff) {
+        *best_out = best;
+        *rank_out = best_rank;
+    }
+    return *rank_out >= 0;
+}
+
+static rt_hit bvh4_intersect(const orc_bvh4 *B, const rt_scene_desc *sc, const rt_aabb *scene_box,
+                             const rt_ray *ray, orc_tests *ct) {
+    rt_hit hit;
+    hit.type = 0; hit.index = -1; hit.mesh_index = -1;
+    hit.distance = FLT_MAX;
+    float best;
+    int r;
+    if (!bvh4_query(B, sc, scene_box, ray, 0, 0.0f, 0.0f, &best, &r, ct)) return hit;
+    hit.distance = best;
+    if (r < B->mt) {
+        const int m = B->mesh_of[r];
+        hit.type = 3; hit.mesh_index = m; hit.index = r - sc->meshes[m].first_triangle;
+    } else if (r < B->mt + B->ns) {
+        hit.type = 1; hit.index = r - B->mt;
+    } else {
+        hit.type = 2; hit.index = r - B->mt - B->ns;
+    }
+    return hit;
+}
+
 typedef struct {
     const rt_scene_desc *sc;
     rt_aabb scene_box;
     f3 bg255;          /* new Rgb(BackgroundColor) = float3(r,g,b) * 255f, Rgb.cs:15-18 */
     int max_bounces;
     const orc_bvh *bvh; /* null: the reference's brute-force scan */
+    const orc_bvh4 *bvh4; /* non-null: the GPU's tree (closest hits; shadow rays any-hit) */
 } frame_t;
 
 static rt_hit trace(const frame_t *fr, const rt_ray *ray, orc_tests *ct) {
+    if (fr->bvh4) return bvh4_intersect(fr->bvh4, fr->sc, &fr->scene_box, ray, ct);
     return fr->bvh ? bvh_intersect(fr->bvh, fr->sc, &fr->scene_box, ray, ct)
                    : intersect(fr->sc, &fr->scene_box, ray, ct);
 }
@@ -474,12 +655,20 @@ static f3 shade(const frame_t *fr, rt_ray ray, int bounce, orc_counts *cnt) {
         rt_ray shadow;
         shadow.origin = add(p, muls(n, SHADOW_RAY_EPSILON));
         shadow.direction = light_dir;
-        rt_hit sh = trace(fr, &shadow, &ct);
         cnt->shadow_rays++;
         float light_dist_sq = distancesq(p, pl->position);
-        if (sh.type != 0) {
-            float hd2 = sh.distance * sh.distance;
-            if (hd2 < light_dist_sq) continue;
+        if (fr->bvh4) { /* any-hit on the GPU's tree: the same predicate (t >= 0, so t*t is monotone) */
+            float bt;
+            int br;
+            if (bvh4_query(fr->bvh4, sc, &fr->scene_box, &shadow, 1, sqrtf(light_dist_sq) * 1.001f, light_dist_sq, &bt,
+                           &br, &ct))
+                continue;
+        } else {
+            rt_hit sh = trace(fr, &shadow, &ct);
+            if (sh.type != 0) {
+                float hd2 = sh.distance * sh.distance;
+                if (hd2 < light_dist_sq) continue;
+            }
         }
         f3 irr = divs(pl->intensity, light_dist_sq);
         /* CalculateDiffuse :443-455: diffuse * max(0, dot(L, N)) * E */
@@ -545,6 +734,7 @@ static int setup(frame_t *fr, const rt_scene_desc *sc, const rt_image_plane *pla
     if (n < 0) return RT_E_INVALID;
     fr->sc = sc;
     fr->bvh = NULL;
+    fr->bvh4 = NULL;
     orc_scene_aabb(sc, &fr->scene_box);
     fr->bg255 = muls(V(prm->background_color[0], prm->background_color[1], prm->background_color[2]), 255.0f);
     fr->max_bounces = prm->max_reflection_bounces;
@@ -561,24 +751,31 @@ static f3 top_left_of(const rt_camera *cam, const rt_image_plane *plane) {
 }
 
 /* Render the pixels listed in pix_idx (x + y*res_x) into out (4 floats each). */
-static int render_pixels(const orc_bvh *bvh, const rt_scene_desc *sc, const rt_camera *cam,
+static int render_pixels(const orc_bvh *bvh, const orc_bvh4 *bvh4, const rt_scene_desc *sc, const rt_camera *cam,
                          const rt_image_plane *plane, const rt_render_params *prm, const int32_t *pix_idx,
                          int32_t npix, float *out, orc_counts *counts, int32_t threads);
 
 int orc_render_pixels(const rt_scene_desc *sc, const rt_camera *cam, const rt_image_plane *plane,
                       const rt_render_params *prm, const int32_t *pix_idx, int32_t npix,
                       float *out, orc_counts *counts, int32_t threads) {
-    return render_pixels(NULL, sc, cam, plane, prm, pix_idx, npix, out, counts, threads);
+    return render_pixels(NULL, NULL, sc, cam, plane, prm, pix_idx, npix, out, counts, threads);
+}
+
+/* The same pixels through the GPU's own 4-wide BVH (orc_bvh4_create). */
+int orc_render_pixels_bvh4(const void *bvh4, const rt_scene_desc *sc, const rt_camera *cam,
+                           const rt_image_plane *plane, const rt_render_params *prm, const int32_t *pix_idx,
+                           int32_t npix, float *out, orc_counts *counts, int32_t threads) {
+    return render_pixels(NULL, (const orc_bvh4 *)bvh4, sc, cam, plane, prm, pix_idx, npix, out, counts, threads);
 }
 
 /* The same pixels with closest hits through a CPU BVH (orc_bvh_build over sc). */
 int orc_render_pixels_bvh(const void *bvh, const rt_scene_desc *sc, const rt_camera *cam,
                           const rt_image_plane *plane, const rt_render_params *prm, const int32_t *pix_idx,
                           int32_t npix, float *out, orc_counts *counts, int32_t threads) {
-    return render_pixels((const orc_bvh *)bvh, sc, cam, plane, prm, pix_idx, npix, out, counts, threads);
+    return render_pixels((const orc_bvh *)bvh, NULL, sc, cam, plane, prm, pix_idx, npix, out, counts, threads);
 }
 
-static int render_pixels(const orc_bvh *bvh, const rt_scene_desc *sc, const rt_camera *cam,
+static int render_pixels(const orc_bvh *bvh, const orc_bvh4 *bvh4, const rt_scene_desc *sc, const rt_camera *cam,
                          const rt_image_plane *plane, const rt_render_params *prm, const int32_t *pix_idx,
                          int32_t npix, float *out, orc_counts *counts, int32_t threads) {
     frame_t fr;
@@ -586,6 +783,7 @@ static int render_pixels(const orc_bvh *bvh, const rt_scene_desc *sc, const rt_c
     int st = setup(&fr, sc, plane, prm, &n);
     if (st) return st;
     fr.bvh = bvh;
+    fr.bvh4 = bvh4;
     f3 tl = top_left_of(cam, plane);
     float hl = plane->half_horizontal_length * 2.0f; /* HorizontalLength, ImagePlane.cs:23 */
     float vl = plane->half_vertical_length * 2.0f;

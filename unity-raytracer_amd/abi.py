@@ -13,7 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "librt_mi355.so")
 
-RT_ABI_VERSION = 3
+RT_ABI_VERSION = 4
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -191,6 +191,11 @@ class rt_ray(C.Structure):
     _fields_ = [("origin", rt_float3), ("direction", rt_float3)]
 
 
+class rt_bvh_export_info(C.Structure):
+    _fields_ = [("nodes", C.c_int32), ("triangle_records", C.c_int32), ("sphere_records", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 # Every entry point declared in include/rt_mi355.h: name -> (restype, argtypes)
 _P = C.c_void_p
 SIGNATURES = {
@@ -204,6 +209,7 @@ SIGNATURES = {
     "rt_set_scene": (C.c_int, [_P, C.POINTER(rt_scene_desc)]),
     "rt_set_scene_ex": (C.c_int, [_P, C.POINTER(rt_scene_desc), C.c_int32]),
     "rt_get_scene_info": (C.c_int, [_P, C.POINTER(rt_scene_info)]),
+    "rt_export_bvh": (C.c_int, [_P, _P, _P, _P, C.POINTER(rt_bvh_export_info)]),
     "rt_set_scene_source": (C.c_int, [_P, C.POINTER(rt_scene_desc), _P, C.c_int32]),
     "rt_update_mesh_transforms": (C.c_int, [_P, _P, C.c_int32]),
     "rt_render": (C.c_int, [_P, C.POINTER(rt_camera), C.POINTER(rt_image_plane),

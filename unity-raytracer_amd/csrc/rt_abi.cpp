@@ -2032,6 +2032,33 @@ int rt_get_scene_info(const rt_ctx *ctx, rt_scene_info *info) {
     return RT_OK;
 }
 
+int rt_export_bvh(const rt_ctx *ctx, void *nodes, void *triangle_records, void *sphere_records,
+                  rt_bvh_export_info *info) {
+    if (!ctx || !info) return RT_E_INVALID;
+    if (!ctx->has_scene) return RT_E_STATE;
+    std::memset(info, 0, sizeof *info);
+    if (ctx->info.primitives > 0 && !ctx->S.bvh4) return RT_E_STATE;
+    const int P = ctx->info.primitives;
+    info->nodes = P > 0 ? ctx->info.nodes : 0;
+    info->triangle_records = ctx->mesh_tri_ranks + ctx->loose_count + 1;  // + the sentinel
+    info->sphere_records = ctx->sphere_count;
+    DeviceGuard guard;
+    if (hipSetDevice(ctx->device) != hipSuccess) return RT_E_HIP;
+    if (nodes && info->nodes &&
+        hipMemcpy(nodes, ctx->S.nodes4, sizeof(rtd::BvhNode4) * (size_t)info->nodes, hipMemcpyDeviceToHost) !=
+            hipSuccess)
+        return RT_E_HIP;
+    if (triangle_records && info->triangle_records &&
+        hipMemcpy(triangle_records, ctx->S.tris, sizeof(rtd::TriRec) * (size_t)info->triangle_records,
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return RT_E_HIP;
+    if (sphere_records && info->sphere_records &&
+        hipMemcpy(sphere_records, ctx->S.sphs, sizeof(rtd::SphRec) * (size_t)info->sphere_records,
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return RT_E_HIP;
+    return RT_OK;
+}
+
 int rt_finish(rt_ctx *ctx, rt_stats *stats) {
     if (!ctx) return RT_E_INVALID;
     DeviceGuard guard;

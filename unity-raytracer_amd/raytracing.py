@@ -187,6 +187,18 @@ class Context:
         if sync:
             self._check(self.lib.rt_synchronize(self.h))
 
+    def export_bvh(self):
+        """The scene's 4-wide BVH as it lies in HBM (rt_export_bvh): node,
+        triangle and sphere records as raw bytes (128 / 48 / 32 B each)."""
+        info = abi.rt_bvh_export_info()
+        self._check(self.lib.rt_export_bvh(self.h, None, None, None, C.byref(info)))
+        nodes = np.zeros(info.nodes * 128, np.uint8)
+        tris = np.zeros(info.triangle_records * 48, np.uint8)
+        sphs = np.zeros(info.sphere_records * 32, np.uint8)
+        self._check(self.lib.rt_export_bvh(self.h, nodes.ctypes.data_as(C.c_void_p), tris.ctypes.data_as(C.c_void_p),
+                                           sphs.ctypes.data_as(C.c_void_p), C.byref(info)))
+        return nodes, tris, sphs
+
     def intersect_rays(self, rays: np.ndarray) -> np.ndarray:
         """Scene.IntersectRay (Scene.cs:43-122) for (N, 6) float32 rays;
         returns a structured array (type, index, mesh_index, distance)."""
