@@ -4,11 +4,11 @@
 // MI355X library.  SOURCE ONLY (no Mono/Unity in the build image).
 //
 // Per frame the component uploads only what changed:
-//   * mesh vertex/index buffers once (rt_set_scene_source), then the
-//     localToWorld matrices every Update (rt_update_mesh_transforms, 64 B per
-//     mesh) — extraction and the BVH rebuild run on the GPU;
-//   * loose triangles, spheres and lights are re-fetched like the reference
-//     (FindObjectsOfType) and, when they change, the scene is re-sent.
+//   * every field the reference's Fetch* methods read is re-read each Update
+//     (as the reference does) and compared byte for byte with the last copy;
+//     any change re-sends the scene source (rt_set_scene_source);
+//   * otherwise only the localToWorld matrices (rt_update_mesh_transforms,
+//     64 B per mesh) — extraction and the BVH rebuild run on the GPU.
 // PixelColors keeps the reference's Color[] (float RGBA, RT_FLAG_OUT default);
 // set OutputRgba8 to receive Color32[] for a Texture2D instead (4x fewer
 // bytes over PCIe).
@@ -17,6 +17,7 @@ using System.Collections.Generic;
 using System.Linq;
 using System.Runtime.InteropServices;
 using Unity.Mathematics;
+// MemoryMarshal / ReadOnlySpan: .NET Standard 2.1 (Unity 2021.3)
 using UnityEngine;
 
 namespace RayTracer.Native
@@ -35,10 +36,7 @@ namespace RayTracer.Native
         public RtStats LastStats;
 
         IntPtr _rt;
-        SceneMesh[] _meshes = Array.Empty<SceneMesh>();
-        UnityEngine.Mesh[] _sharedMeshes = Array.Empty<UnityEngine.Mesh>();
         RtMatrix[] _matrices = Array.Empty<RtMatrix>();
-        int _staticHash;
 
         void Start()
         {
@@ -67,8 +65,38 @@ namespace RayTracer.Native
             CastPixelRays(cameraData);
         }
 
-        // UpdateScene (:120-128): re-send the scene when its object set or a
-        // static object changed; otherwise only the mesh transforms.
+        // UpdateScene (:120-128).  Every Update re-reads exactly what the
+        // reference's Fetch* methods read (FetchTriangles :159-169 -> SceneTriangle
+        // position + Offset0/1/2 + Material; FetchSpheres -> SceneSphere position,
+        // localScale.x, Material; FetchMeshes -> SceneMesh sharedMesh, vertices,
+        // triangles, localToWorldMatrix, Material; FetchPointLights ->
+        // ScenePointLight position + Intensity; FetchAmbientLights ->
+        // SceneAmbientLight.AmbientLight) and compares it byte for byte with the
+        // previous Update's copy; on any difference the whole scene source is
+        // re-sent (rt_set_scene_source), otherwise only the mesh matrices
+        // (rt_update_mesh_transforms: device extraction + BVH rebuild).
+        // DetectMeshEdits = false skips re-reading Mesh.vertices / triangles
+        // (the one read whose cost grows with the mesh, as in the reference):
+        // then an in-place edit of a shared mesh's vertex or index buffer is
+        // NOT seen — Unity keeps no cheap version counter on a Mesh.
+        public bool DetectMeshEdits = true;
+
+        StaticScene _static;
+
+        struct StaticScene
+        {
+            public Triangle[] Tris;
+            public RtMaterial[] TriMats, SphMats, MeshMats;
+            public Sphere[] Spheres;
+            public PointLightData[] Lights;
+            public float3 Ambient;
+            public int AmbientCount;
+            public SceneMesh[] Meshes;
+            public UnityEngine.Mesh[] SharedMeshes;
+            public Vector3[][] Vertices;
+            public int[][] Indices;
+        }
+
         void UpdateScene()
         {
             var meshes = FindObjectsOfType<SceneMesh>();
@@ -78,11 +106,26 @@ namespace RayTracer.Native
             var ambient = FindObjectsOfType<SceneAmbientLight>();
             if (ambient.Length > 1) Debug.LogError("There are more than Single Ambient Lights in the Scene.");
 
-            int hash = StaticHash(tris, spheres, lights, ambient);
-            bool sameMeshes = meshes.Length == _meshes.Length &&
-                              meshes.Select(m => m.MeshFilter.sharedMesh).SequenceEqual(_sharedMeshes) &&
-                              meshes.SequenceEqual(_meshes);
-            if (sameMeshes && hash == _staticHash)
+            var cur = new StaticScene
+            {
+                Tris = tris.Select(t => t.Triangle).ToArray(),
+                TriMats = tris.Select(t => Rt.Material(t.Material)).ToArray(),
+                Spheres = spheres.Select(x => x.Sphere).ToArray(),
+                SphMats = spheres.Select(x => Rt.Material(x.Material)).ToArray(),
+                Lights = lights.Select(l => l.Light).ToArray(),
+                // FetchAmbientLights (:130-147): more than one -> logged, none used
+                Ambient = ambient.Length == 1 ? ambient[0].AmbientLight.Radiance : float3.zero,
+                AmbientCount = ambient.Length,
+                Meshes = meshes,
+                SharedMeshes = meshes.Select(m => m.MeshFilter.sharedMesh).ToArray(),
+                MeshMats = meshes.Select(m => Rt.Material(m.Material)).ToArray(),
+            };
+            if (DetectMeshEdits)
+            {
+                cur.Vertices = cur.SharedMeshes.Select(m => m.vertices).ToArray();
+                cur.Indices = cur.SharedMeshes.Select(m => m.triangles).ToArray();
+            }
+            if (SameScene(cur, _static))
             {
                 for (int i = 0; i < meshes.Length; i++)
                     _matrices[i] = RtMatrix.FromUnity(meshes[i].transform.localToWorldMatrix);
@@ -90,12 +133,38 @@ namespace RayTracer.Native
                     Debug.LogError(Rt.LastError(_rt));
                 return;
             }
-            SetSceneSource(meshes, tris, spheres, lights, ambient.Length == 1 ? ambient[0] : null);
-            _staticHash = hash;
+            SetSceneSource(cur);
+            _static = cur;
         }
 
-        void SetSceneSource(SceneMesh[] meshes, SceneTriangle[] tris, SceneSphere[] spheres,
-                            ScenePointLight[] lights, SceneAmbientLight ambient)
+        // Byte-for-byte equality of two blittable arrays (float bits: a sign
+        // of zero or a NaN payload change counts, as it can change the image).
+        static bool SameBytes<T>(T[] a, T[] b) where T : unmanaged
+        {
+            if (a == null || b == null) return a == b;
+            return MemoryMarshal.AsBytes(new ReadOnlySpan<T>(a)).SequenceEqual(MemoryMarshal.AsBytes(new ReadOnlySpan<T>(b)));
+        }
+
+        static bool SameScene(in StaticScene a, in StaticScene b)
+        {
+            if (b.Meshes == null) return false;  // first Update
+            if (!SameBytes(a.Tris, b.Tris) || !SameBytes(a.TriMats, b.TriMats) || !SameBytes(a.Spheres, b.Spheres) ||
+                !SameBytes(a.SphMats, b.SphMats) || !SameBytes(a.Lights, b.Lights) ||
+                !SameBytes(new[] { a.Ambient }, new[] { b.Ambient }) || a.AmbientCount != b.AmbientCount ||
+                !SameBytes(a.MeshMats, b.MeshMats))
+                return false;
+            if (!a.Meshes.SequenceEqual(b.Meshes) || !a.SharedMeshes.SequenceEqual(b.SharedMeshes)) return false;
+            if (a.Vertices != null)
+            {
+                if (b.Vertices == null) return false;
+                for (int i = 0; i < a.Vertices.Length; i++)
+                    if (!SameBytes(a.Vertices[i], b.Vertices[i]) || !SameBytes(a.Indices[i], b.Indices[i]))
+                        return false;
+            }
+            return true;
+        }
+
+        void SetSceneSource(in StaticScene sc)
         {
             var handles = new List<GCHandle>();
             IntPtr Pin(Array a)
@@ -108,39 +177,34 @@ namespace RayTracer.Native
             try
             {
                 // FetchTriangles / FetchSpheres / FetchPointLights / FetchAmbientLights
-                var triArr = tris.Select(t => t.Triangle).ToArray();
                 var desc = new RtSceneDesc
                 {
-                    Triangles = Pin(triArr),
-                    TriangleNormals = Pin(triArr.Select(t => t.Normal).ToArray()),
-                    TriangleMaterials = Pin(tris.Select(t => Rt.Material(t.Material)).ToArray()),
-                    TriangleCount = triArr.Length,
-                    Spheres = Pin(spheres.Select(s => s.Sphere).ToArray()),
-                    SphereMaterials = Pin(spheres.Select(s => Rt.Material(s.Material)).ToArray()),
-                    SphereCount = spheres.Length,
-                    PointLights = Pin(lights.Select(l => l.Light).ToArray()),
-                    PointLightCount = lights.Length,
-                    AmbientRadiance = ambient != null ? ambient.AmbientLight.Radiance : float3.zero,
+                    Triangles = Pin(sc.Tris),
+                    TriangleNormals = Pin(sc.Tris.Select(t => t.Normal).ToArray()),
+                    TriangleMaterials = Pin(sc.TriMats),
+                    TriangleCount = sc.Tris.Length,
+                    Spheres = Pin(sc.Spheres),
+                    SphereMaterials = Pin(sc.SphMats),
+                    SphereCount = sc.Spheres.Length,
+                    PointLights = Pin(sc.Lights),
+                    PointLightCount = sc.Lights.Length,
+                    AmbientRadiance = sc.Ambient,
                 };
                 // SceneMesh sources: local vertices + index buffer + transform
-                var src = new RtMeshSource[meshes.Length];
-                _sharedMeshes = new UnityEngine.Mesh[meshes.Length];
-                _matrices = new RtMatrix[meshes.Length];
-                for (int i = 0; i < meshes.Length; i++)
+                var src = new RtMeshSource[sc.Meshes.Length];
+                _matrices = new RtMatrix[sc.Meshes.Length];
+                for (int i = 0; i < sc.Meshes.Length; i++)
                 {
-                    var um = meshes[i].MeshFilter.sharedMesh;
-                    var verts = um.vertices;
-                    var idx = um.triangles;
-                    _sharedMeshes[i] = um;
-                    _matrices[i] = RtMatrix.FromUnity(meshes[i].transform.localToWorldMatrix);
+                    var verts = sc.Vertices != null ? sc.Vertices[i] : sc.SharedMeshes[i].vertices;
+                    var idx = sc.Indices != null ? sc.Indices[i] : sc.SharedMeshes[i].triangles;
+                    _matrices[i] = RtMatrix.FromUnity(sc.Meshes[i].transform.localToWorldMatrix);
                     src[i] = new RtMeshSource
                     {
                         Vertices = Pin(verts), VertexCount = verts.Length,
                         Indices = Pin(idx), IndexCount = idx.Length,
-                        LocalToWorld = _matrices[i], Material = Rt.Material(meshes[i].Material),
+                        LocalToWorld = _matrices[i], Material = sc.MeshMats[i],
                     };
                 }
-                _meshes = meshes;
                 if (Rt.rt_set_scene_source(_rt, ref desc, src, src.Length) != Rt.OK)
                     Debug.LogError(Rt.LastError(_rt));
             }
@@ -148,16 +212,6 @@ namespace RayTracer.Native
             {
                 foreach (var h in handles) h.Free();
             }
-        }
-
-        static int StaticHash(SceneTriangle[] t, SceneSphere[] s, ScenePointLight[] l, SceneAmbientLight[] a)
-        {
-            var h = new HashCode();
-            foreach (var x in t) { h.Add(x.GetInstanceID()); h.Add(x.transform.position); }
-            foreach (var x in s) { h.Add(x.GetInstanceID()); h.Add(x.transform.position); h.Add(x.transform.localScale); }
-            foreach (var x in l) { h.Add(x.GetInstanceID()); h.Add(x.transform.position); h.Add(x.Intensity); }
-            foreach (var x in a) h.Add(x.GetInstanceID());
-            return h.ToHashCode();
         }
 
         // CastPixelRays (:275-302)

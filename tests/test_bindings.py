@@ -46,3 +46,52 @@ def test_shim_struct_field_counts(rt):
             continue
         assert len(got) == len(ct._fields_), (cs, got)
     assert len(_cs_fields("RtMatrix")) == 16
+
+
+SETUP = os.path.join(ROOT, "bindings", "csharp", "RayTracingSetupNative.cs")
+
+# Every value the reference's per-Update scene fetch reads
+# (RayTracingSetup.cs:120-169 and the SceneComponents getters), with the
+# expression through which the shim reads it and the field of its StaticScene
+# snapshot that carries it into the byte-for-byte change test.
+REFERENCE_READS = [
+    ("SceneTriangle.Triangle: position + Offset0/1/2 (SceneTriangle.cs:16-22)", "t.Triangle", "Tris"),
+    ("SceneTriangle.Material (SceneTriangle.cs:12, FetchTriangles :166)", "Rt.Material(t.Material)", "TriMats"),
+    ("SceneSphere.Sphere: position, localScale.x (SceneSphere.cs:9-22)", "x.Sphere", "Spheres"),
+    ("SceneSphere.Material (SceneSphere.cs:7)", "Rt.Material(x.Material)", "SphMats"),
+    ("ScenePointLight.Light: position + Intensity (ScenePointLight.cs:9-13)", "l.Light", "Lights"),
+    ("SceneAmbientLight.AmbientLight (SceneAmbientLight.cs:7, :130-147)", "AmbientLight.Radiance", "Ambient"),
+    ("number of ambient lights (:135-139)", "ambient.Length", "AmbientCount"),
+    ("SceneMesh.MeshFilter.sharedMesh (SceneMesh.cs:15)", "m.MeshFilter.sharedMesh", "SharedMeshes"),
+    ("Mesh.vertices (SceneMesh.cs:16)", "m.vertices", "Vertices"),
+    ("Mesh.triangles (SceneMesh.cs:17)", "m.triangles", "Indices"),
+    ("SceneMesh.Material (SceneMesh.cs:9)", "Rt.Material(m.Material)", "MeshMats"),
+    ("the SceneMesh objects (FindObjectsOfType order)", "Meshes = meshes", "Meshes"),
+]
+
+
+def _method(src, name):
+    i = src.index(name)
+    j = src.index("{", i)
+    depth, k = 0, j
+    while True:
+        depth += {"{": 1, "}": -1}.get(src[k], 0)
+        if depth == 0:
+            return src[j:k + 1]
+        k += 1
+
+
+def test_shim_change_detection_covers_every_reference_read():
+    """The shim re-sends the scene whenever anything the reference re-reads
+    every Update changed: each read appears in UpdateScene's snapshot and each
+    snapshot field in SameScene's comparison (localToWorldMatrix is uploaded
+    every frame through rt_update_mesh_transforms)."""
+    src = open(SETUP).read()
+    update = _method(src, "void UpdateScene()")
+    same = _method(src, "static bool SameScene(")
+    for what, expr, field in REFERENCE_READS:
+        assert expr in update, what
+        assert f"a.{field}" in same and f"b.{field}" in same, what
+    assert "localToWorldMatrix" in update and "rt_update_mesh_transforms" in update
+    # byte-for-byte comparison (float bits), not float equality
+    assert "MemoryMarshal.AsBytes" in src
