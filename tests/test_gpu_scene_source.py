@@ -138,10 +138,16 @@ def test_update_equals_fresh_source_scene(gpu_ctx, rt):
     gpu_ctx.set_scene_source(fr.scene, srcs)
     gpu_ctx.update_mesh_transforms(mats(0.8))
     a, sa = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+    tree_a = gpu_ctx.export_bvh()
     moved = [rt.MeshSource(s.Vertices, s.Indices, m, s.MaterialData) for s, m in zip(srcs, mats(0.8))]
     gpu_ctx.set_scene_source(fr.scene, moved)
     b, sb = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
     assert _same(a, b) and _counts(sa) == _counts(sb)
+    # the update folds the scene box and its padding on the device
+    # (k_scene_box); the host computes them for a fresh scene: same bits,
+    # hence the same sort keys, padded boxes and tree
+    for x, y in zip(tree_a, gpu_ctx.export_bvh()):
+        assert np.array_equal(x, y)
 
 
 def test_source_errors(gpu_ctx, rt):

@@ -14,6 +14,8 @@ namespace rtk {
 size_t tile_sort_scratch_bytes(int n);
 // waves of a render_kernel launch of F (tiles + the extra waves of split tiles)
 int render_mega_waves(const rtd::FrameDev &F);
+// Sums the kCounterSlots sharded counter slots into kCounterWords words at out.
+hipError_t launch_fold_counters(const unsigned long long *counters, unsigned long long *out, hipStream_t stream);
 hipError_t launch_iota(int *p, int n, hipStream_t stream);
 hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const int *iota, int *order, int n,
                               void *scratch, size_t scratch_bytes, hipStream_t stream);

@@ -49,6 +49,7 @@ struct LbvhInput {
     const int *loose_mat;             // nl
     float scene_lo[3], scene_hi[3];   // Scene.AABB (quantisation box)
     float pad_abs;                    // same padding as the host builder
+    const float *box_dev;             // non-null: {scene_lo, scene_hi, pad_abs} from device memory instead
     const rtd::MeshGate *gates;       // mesh_count exact mesh AABBs (Mesh.AABB, the gates)
     int mesh_bits;                    // bits of (mesh id + 1) in the sort key
     int key_bits;                     // 64: 30-bit Morton | mesh id + 1 | in-mesh Morton

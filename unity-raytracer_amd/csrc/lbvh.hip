@@ -45,6 +45,20 @@ __global__ void k_prims(LbvhInput in, LbvhOutput out, int n, float4 *plo, float4
                         int *vals, rtd::TriRec *tri_rank) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
+    float scene_lo[3], scene_hi[3], pad_abs;
+    if (in.box_dev) {  // computed on the device this frame (scene_xform.hip k_scene_box)
+        for (int a = 0; a < 3; ++a) {
+            scene_lo[a] = in.box_dev[a];
+            scene_hi[a] = in.box_dev[3 + a];
+        }
+        pad_abs = in.box_dev[6];
+    } else {
+        for (int a = 0; a < 3; ++a) {
+            scene_lo[a] = in.scene_lo[a];
+            scene_hi[a] = in.scene_hi[a];
+        }
+        pad_abs = in.pad_abs;
+    }
     float lo[3], hi[3], cen[3];
     int gate = -1;
     if (r < in.mt || r >= in.mt + in.ns) {
@@ -84,7 +98,7 @@ __global__ void k_prims(LbvhInput in, LbvhOutput out, int n, float4 *plo, float4
             hi[a] = fmaxf(vs[0][a], fmaxf(vs[1][a], vs[2][a]));
             ext = fmaxf(ext, hi[a] - lo[a]);
         }
-        const float pad = in.pad_abs + ext * 1e-4f;
+        const float pad = pad_abs + ext * 1e-4f;
         for (int a = 0; a < 3; ++a) {
             cen[a] = 0.5f * (lo[a] + hi[a]);
             lo[a] -= pad;
@@ -99,7 +113,7 @@ __global__ void k_prims(LbvhInput in, LbvhOutput out, int n, float4 *plo, float4
         sr.misc = make_int4(r, -1, 0, 0);
         *(rtd::SphRec *)&tri_rank[r] = sr;
         out.shade[r] = make_float4(sp[0], sp[1], sp[2], __int_as_float(in.sphere_mat[i]));
-        const float pad = in.pad_abs + rad * 1e-4f;
+        const float pad = pad_abs + rad * 1e-4f;
         for (int a = 0; a < 3; ++a) {
             cen[a] = sp[a];
             lo[a] = sp[a] - rad - pad;
@@ -123,10 +137,10 @@ __global__ void k_prims(LbvhInput in, LbvhOutput out, int n, float4 *plo, float4
         const int low_bits = 34 - in.mesh_bits;
         const int per_axis = low_bits >= 30 ? 10 : low_bits / 3;
         const unsigned long long low = per_axis > 0 ? morton(c, mlo, mhi, per_axis) : 0ull;
-        key = ((unsigned long long)morton(mc, in.scene_lo, in.scene_hi, 10) << 34) |
+        key = ((unsigned long long)morton(mc, scene_lo, scene_hi, 10) << 34) |
               ((unsigned long long)(gate + 1) << low_bits) | low;
     } else {
-        key = (unsigned long long)morton(c, in.scene_lo, in.scene_hi, 10) << 34;
+        key = (unsigned long long)morton(c, scene_lo, scene_hi, 10) << 34;
     }
     keys[r] = key;
     vals[r] = r;

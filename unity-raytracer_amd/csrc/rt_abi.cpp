@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -20,6 +21,10 @@
 #include <vector>
 
 #include <dlfcn.h>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 #include <hip/hip_runtime.h>
@@ -46,10 +51,11 @@ struct LbvhBufs {
     GrowBuf nodes, nodes4, tris, sphs, shade, scratch;
     // device mesh extraction (scene_xform.hip): resident sources + matrices
     GrowBuf src_meshes, src_local, src_indices, src_matrices, src_world, src_aabbs, src_parts;
+    GrowBuf scene_box;  // {lo[3], hi[3], pad_abs} of an animated scene (scene_xform.hip k_scene_box)
     void release() {
         GrowBuf *all[] = {&meshes, &mesh_tris, &mesh_normals, &spheres, &sphere_mat, &loose_tris, &loose_normals,
                           &loose_mat, &nodes, &nodes4, &tris, &sphs, &shade, &scratch, &src_meshes, &src_local,
-                          &src_indices, &src_matrices, &src_world, &src_aabbs, &src_parts};
+                          &src_indices, &src_matrices, &src_world, &src_aabbs, &src_parts, &scene_box};
         for (GrowBuf *b : all) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
@@ -105,6 +111,77 @@ struct GroupSlot {
     std::vector<GrowBuf> member_out;         // per member: its band, on its device
     GrowBuf gather;                          // device 0: every band back to back
     hipEvent_t gather_free = nullptr;        // device 0: the last frame's bands are reassembled
+};
+
+// rt_render's host-output copies, issued from a thread of their own: a copy
+// into pageable memory holds the calling thread until it is done, so the
+// thread that enqueues the slab launches must not be the one that copies — the
+// first slab's copy then starts as soon as that slab is rendered.
+struct Copier {
+    struct Job {
+        hipEvent_t ready;  // the slab's launch has ended
+        void *dst;
+        const void *src;
+        size_t bytes;
+    };
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv, done_cv;
+    std::deque<Job> jobs;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool quit = false, busy = false;
+    hipError_t err = hipSuccess;
+
+    void start(int dev, hipStream_t s) {
+        device = dev;
+        stream = s;
+        th = std::thread([this] { run(); });
+    }
+    void run() {
+        (void)hipSetDevice(device);
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+            cv.wait(lk, [this] { return quit || !jobs.empty(); });
+            if (jobs.empty()) return;  // quit
+            const Job j = jobs.front();
+            jobs.pop_front();
+            busy = true;
+            lk.unlock();
+            // the copy stream waits for the slab on the device; a pageable
+            // copy returns once it is done
+            hipError_t e = hipStreamWaitEvent(stream, j.ready, 0);
+            if (e == hipSuccess) e = hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToHost, stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            lk.lock();
+            if (e != hipSuccess && err == hipSuccess) err = e;
+            busy = false;
+            if (jobs.empty()) done_cv.notify_all();
+        }
+    }
+    void post(const Job &j) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            jobs.push_back(j);
+        }
+        cv.notify_one();
+    }
+    hipError_t wait() {  // every posted copy is done; returns (and clears) the first error
+        std::unique_lock<std::mutex> lk(mu);
+        done_cv.wait(lk, [this] { return jobs.empty() && !busy; });
+        const hipError_t e = err;
+        err = hipSuccess;
+        return e;
+    }
+    void stop() {
+        if (!th.joinable()) return;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+        }
+        cv.notify_all();
+        th.join();
+    }
 };
 
 // RCCL, resolved at run time (only a multi-device context with an RCCL gather
@@ -186,6 +263,13 @@ struct rt_ctx {
     float4 *d_out = nullptr;
     size_t d_out_cap = 0;
     unsigned long long *d_counters = nullptr;
+    unsigned long long *h_counts = nullptr;  // page-locked: the folded counters (fold_counters_kernel)
+    // page-locked results of rt_update_mesh_transforms' one synchronisation
+    struct UpdateHost {
+        float box[8];  // lo[3], hi[3], pad_abs
+        int binfo[4];  // lbvh_info_ptr: 2-wide depth, 4-wide nodes, 4-wide depth
+    } *h_update = nullptr;
+    hipEvent_t ev_x = nullptr;  // end of the device extraction in an update
     float *d_rays = nullptr;
     int4 *d_hits = nullptr;
     size_t rays_cap = 0;
@@ -219,6 +303,7 @@ struct rt_ctx {
     std::vector<std::pair<hipStream_t, hipEvent_t>> async_end;
     // rt_render's slab pipeline: copy stream + one event per slab
     hipStream_t copy_stream = nullptr;
+    Copier copier;  // its thread runs only after a context's first host-output frame
     std::vector<hipEvent_t> slab_done;
     hipStream_t slab_stream2 = nullptr;  // ... odd slabs render here, even ones on the context's stream
     // multi-device context: this context is member 0 (the root, device 0 of
@@ -555,19 +640,31 @@ constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this
 constexpr int kSplit16MaxTiles = 70000;
 constexpr int kSplit16DivLarge = 4096;
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
-// rt_render's host-output pipeline: about this many bytes per row slab, at most kMaxSlabs slabs (C3:
-// 8 slabs of 4.1 MB in float RGBA, 4 of 2.1 MB in RGBA8), alternating over two streams
-constexpr size_t kSlabBytes = (size_t)2 << 20;
-constexpr int kMaxSlabs = 8;
+// rt_render's host-output pipeline: row slabs of about kSlabBytes, 3 to 8 of them (C3 at 1080p: 8
+// slabs of 4.1 MB in float RGBA, 3 of 2.8 MB in RGBA8; measured best, tools/exp/e2e_sweep.py),
+// alternating over two streams; frames under kSlabMinFrame in one piece
+constexpr size_t kSlabBytes = (size_t)4 << 20;
+constexpr size_t kSlabMinFrame = (size_t)2 << 20;
+constexpr int kMaxSlabs = 16;  // RT_SLABS (tuning) range
 
-// Sums the sharded ray/test counters on the host (the stream must be idle).
+// Enqueues the sum of the sharded ray/test counters into ctx->h_counts (read
+// after the stream's synchronisation by read_folded).
+int fold_counters(rt_ctx *ctx, hipStream_t stream) {
+    HIP_OR_FAIL(ctx, rtk::launch_fold_counters(ctx->d_counters, ctx->h_counts, stream));
+    return RT_OK;
+}
+
+void read_folded(const rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
+    const volatile unsigned long long *h = ctx->h_counts;
+    for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] = h[w];
+}
+
+// Sums the sharded ray/test counters (the counters' frames must have ended).
 int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
-    const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
-    std::vector<unsigned long long> slots((size_t)rtd::kCounterSlots * rtd::kCounterWords);
-    HIP_OR_FAIL(ctx, hipMemcpy(slots.data(), ctx->d_counters, ctr_bytes, hipMemcpyDeviceToHost));
-    for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] = 0;
-    for (int sl = 0; sl < rtd::kCounterSlots; ++sl)
-        for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] += slots[(size_t)sl * rtd::kCounterWords + w];
+    int st = fold_counters(ctx, ctx->stream);
+    if (st) return st;
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    read_folded(ctx, counts);
     return RT_OK;
 }
 
@@ -669,10 +766,9 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     if (ls->scene != ctx->scene_version) {
         // a new or updated scene (rt_update_mesh_transforms every Update): the
         // last order stays a valid permutation of the tiles and, animation being
-        // temporally coherent, a good one — keep dispatching by it and measure
-        // this frame's costs for the next
+        // temporally coherent, a good one — keep dispatching by it and keep the
+        // re-sort period (re-sorting after every update cost ~55 us a frame)
         ls->scene = ctx->scene_version;
-        ls->frames = 0;
     }
     if (!ls->valid) ls->frames = 0;
     F.tile_order = ls->valid ? (const int *)ls->order.p : nullptr;
@@ -788,7 +884,10 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     // outside the timed region, which covers device work only
     if (slabs) {
         row_bytes = (int)(out_bytes / (size_t)std::max(1, F.local_rows));
-        const int nslab = std::max(1, std::min(kMaxSlabs, (int)(out_bytes / kSlabBytes)));
+        int nslab = out_bytes < kSlabMinFrame
+                        ? 1
+                        : std::max(3, std::min(8, (int)((out_bytes + kSlabBytes / 2) / kSlabBytes)));
+        if (const char *e = std::getenv("RT_SLABS")) nslab = std::max(1, std::min(kMaxSlabs, std::atoi(e)));  // tuning
         // slab boundaries on whole tile rows
         const int tile_rows = (F.local_rows + F.tile_h - 1) / F.tile_h;
         if (!ctx->copy_stream) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
@@ -839,11 +938,18 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         const int nslab = (int)launches.size();
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_slab0, base));
         HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->slab_stream2, ctx->ev_slab0, 0));
+        if (!ctx->copier.th.joinable()) ctx->copier.start(ctx->device, ctx->copy_stream);
         for (int k = 0; k < nslab; ++k) {
             ctx->stream = launches[k].stream;
             int st = launch_frame(ctx, launches[k].F, P, A, chunk_tiles);
             if (st) return st;
             HIP_OR_FAIL(ctx, hipEventRecord(ctx->slab_done[k], ctx->stream));
+            // the copier thread copies slab k once its launch has ended, while
+            // this thread enqueues the next launches
+            const int r0 = launches[k].r0, r1 = launches[k].r1;
+            if (r1 > r0)
+                ctx->copier.post({ctx->slab_done[k], (char *)host_out + (size_t)r0 * row_bytes,
+                                  (const char *)d_out + (size_t)r0 * row_bytes, (size_t)(r1 - r0) * row_bytes});
         }
         ctx->stream = base;
         if (nslab > 1) HIP_OR_FAIL(ctx, hipStreamWaitEvent(base, ctx->slab_done[nslab - (nslab & 1 ? 2 : 1)], 0));
@@ -855,17 +961,9 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             if (st) return st;
         }
         ctx->stream = base;
-        // every launch is enqueued before the first copy: a copy into pageable
-        // memory may hold the host until it is done
-        for (int k = 0; k < nslab; ++k) {
-            const int r0 = launches[k].r0, r1 = launches[k].r1;
-            if (r1 <= r0) continue;
-            HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->copy_stream, ctx->slab_done[k], 0));
-            HIP_OR_FAIL(ctx, hipMemcpyAsync((char *)host_out + (size_t)r0 * row_bytes,
-                                            (const char *)d_out + (size_t)r0 * row_bytes,
-                                            (size_t)(r1 - r0) * row_bytes, hipMemcpyDeviceToHost, ctx->copy_stream));
-        }
-        HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->copy_stream));
+        int st = fold_counters(ctx, base);  // base has waited for every launch
+        if (st) return st;
+        HIP_OR_FAIL(ctx, ctx->copier.wait());  // every slab is in the caller's buffer
     } else {
         Launch &L = launches[0];
         int st = launch_frame(ctx, L.F, P, A, chunk_tiles);
@@ -885,6 +983,8 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             return RT_OK;
         }
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+        st = fold_counters(ctx, ctx->stream);
+        if (st) return st;
         if (L.sort) {  // after the timed region: the order of the next frames
             st = lpt_sort_now(ctx, L.F, L.ls);
             if (st) return st;
@@ -894,8 +994,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     }
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     unsigned long long counts[rtd::kCounterWords];
-    int st = read_counters(ctx, counts);
-    if (st) return st;
+    read_folded(ctx, counts);
     if (stats) {
         float ms = 0.0f;
         HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -1046,7 +1145,7 @@ int warm_up(rt_ctx *ctx);
 
 // Device mesh extraction from the resident sources (scene_xform.hip); returns
 // the exact per-mesh AABBs on the host (they feed Scene.CalculateAABB).
-int extract_meshes(rt_ctx *ctx, std::vector<rtd::MeshGate> &aabbs, float &ms) {
+rtx::XformArgs xform_args(rt_ctx *ctx) {
     LbvhBufs &B = ctx->lb;
     rtx::XformArgs a{};
     a.mesh_count = ctx->src.mesh_count;
@@ -1062,6 +1161,12 @@ int extract_meshes(rt_ctx *ctx, std::vector<rtd::MeshGate> &aabbs, float &ms) {
     a.aabbs = (rtd::MeshGate *)B.src_aabbs.p;
     a.part_total = ctx->src.part_total;
     a.parts = (rtd::MeshGate *)B.src_parts.p;
+    return a;
+}
+
+int extract_meshes(rt_ctx *ctx, std::vector<rtd::MeshGate> &aabbs, float &ms) {
+    LbvhBufs &B = ctx->lb;
+    const rtx::XformArgs a = xform_args(ctx);
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     HIP_OR_FAIL(ctx, rtx::transform_meshes(a, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
@@ -1104,7 +1209,9 @@ int create_one(int dev, rt_ctx **out) {
         hipEventCreate(&c->ev_a0) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_slab0, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_counters, rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long)) !=
-            hipSuccess) {
+            hipSuccess ||
+        hipHostMalloc((void **)&c->h_counts, rtd::kCounterWords * sizeof(unsigned long long),
+                      hipHostMallocCoherent) != hipSuccess) {
         rt_destroy(c);
         return fail(nullptr, RT_E_HIP, "stream/event/counter allocation failed");
     }
@@ -1115,6 +1222,7 @@ int create_one(int dev, rt_ctx **out) {
 
 void destroy_one(rt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
+    ctx->copier.stop();
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
     if (ctx->slab_stream2) (void)hipStreamSynchronize(ctx->slab_stream2);
@@ -1125,6 +1233,9 @@ void destroy_one(rt_ctx *ctx) {
     if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
+    if (ctx->h_update) (void)hipHostFree(ctx->h_update);
+    if (ctx->ev_x) (void)hipEventDestroy(ctx->ev_x);
     if (ctx->d_rays) (void)hipFree(ctx->d_rays);
     if (ctx->d_hits) (void)hipFree(ctx->d_hits);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -1955,6 +2066,11 @@ int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_s
     return RT_OK;
 }
 
+// The shim's per-Update path: one host synchronisation.  Matrices up,
+// extraction, the scene box (device fold of the mesh AABBs), the mesh gates
+// and the LBVH build are enqueued back to back; the host then reads the box
+// (for the frame's kernel arguments) and the build's depth (the traversal
+// stack check) from page-locked words.
 int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count,
                               std::chrono::steady_clock::time_point t0) {
     if (!ctx->has_scene || !ctx->src.active)
@@ -1964,42 +2080,72 @@ int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
     LbvhBufs &B = ctx->lb;
+    if (!ctx->h_update)
+        HIP_OR_FAIL(ctx, hipHostMalloc((void **)&ctx->h_update, sizeof *ctx->h_update, hipHostMallocCoherent));
+    if (!ctx->ev_x) HIP_OR_FAIL(ctx, hipEventCreate(&ctx->ev_x));
+    HIP_OR_FAIL(ctx, ensure(ctx, B.scene_box, 8 * sizeof(float)));
     ++ctx->scene_version;
-    HIP_OR_FAIL(ctx, put(ctx, B.src_matrices, local_to_world, (size_t)mesh_count * 16));
-    std::vector<rtd::MeshGate> aabbs;
-    float xform_ms = 0.0f;
-    int st = extract_meshes(ctx, aabbs, xform_ms);
-    if (st) return st;
-    // Scene.CalculateAABB: mesh AABBs, then the (unchanged) loose triangles and spheres
-    rtm::f3 smin = rtm::mk(FLT_MAX, FLT_MAX, FLT_MAX), smax = rtm::mk(-FLT_MAX, -FLT_MAX, -FLT_MAX);
-    auto enc_box = [&](float4 lo, float4 hi) {
-        smin = rtm::mk(rtm::umin(smin.x, lo.x), rtm::umin(smin.y, lo.y), rtm::umin(smin.z, lo.z));
-        smax = rtm::mk(rtm::umax(smax.x, hi.x), rtm::umax(smax.y, hi.y), rtm::umax(smax.z, hi.z));
-    };
-    for (const rtd::MeshGate &g : aabbs) enc_box(g.lo, g.hi);
-    enc_box(make_float4(ctx->src.rest_lo[0], ctx->src.rest_lo[1], ctx->src.rest_lo[2], 0.0f),
-            make_float4(ctx->src.rest_hi[0], ctx->src.rest_hi[1], ctx->src.rest_hi[2], 0.0f));
-    if (mesh_count)
-        HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->arr.gates, aabbs.data(), sizeof(rtd::MeshGate) * aabbs.size(),
+    if (mesh_count)  // pageable source: staged before the call returns
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(B.src_matrices.p, local_to_world, sizeof(float) * 16 * (size_t)mesh_count,
                                         hipMemcpyHostToDevice, ctx->stream));
-    rtd::SceneDev &S = ctx->S;
-    ctx->info.build_ms = xform_ms;
+    const rtx::XformArgs a = xform_args(ctx);
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    HIP_OR_FAIL(ctx, rtx::transform_meshes(a, ctx->stream));
+    // Scene.CalculateAABB: mesh AABBs, then the (unchanged) loose triangles and spheres
+    HIP_OR_FAIL(ctx, rtx::scene_box(a.aabbs, mesh_count, ctx->src.rest_lo, ctx->src.rest_hi, (float *)B.scene_box.p,
+                                    ctx->h_update->box, ctx->stream));
+    if (mesh_count)  // the exact mesh gates (Scene.cs:67)
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->arr.gates, a.aabbs, sizeof(rtd::MeshGate) * (size_t)mesh_count,
+                                        hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_x, ctx->stream));
     const int P = ctx->src.in.mt + ctx->src.in.ns + ctx->src.in.nl;
+    LbvhBufs &L = ctx->lb;
+    const bool wide = ctx->src.wide;
     if (P > 0) {
         rtl::LbvhInput in = ctx->src.in;
-        in.scene_lo[0] = smin.x; in.scene_lo[1] = smin.y; in.scene_lo[2] = smin.z;
-        in.scene_hi[0] = smax.x; in.scene_hi[1] = smax.y; in.scene_hi[2] = smax.z;
-        in.pad_abs = pad_abs_of(smin, smax);
-        int nodes = 0;
-        st = run_lbvh(ctx, in, ctx->src.wide, S, nodes);
-        if (st) {
-            ctx->has_scene = false;
-            return st;
-        }
-        ctx->info.nodes = nodes;
+        in.box_dev = (const float *)B.scene_box.p;
+        rtl::LbvhOutput out{};
+        out.nodes = (rtd::BvhNode *)L.nodes.p;
+        out.nodes4 = wide ? (rtd::BvhNode4 *)L.nodes4.p : nullptr;
+        out.tris = (rtd::TriRec *)L.tris.p;
+        out.sphs = (rtd::SphRec *)L.sphs.p;
+        out.shade = (float4 *)L.shade.p;
+        HIP_OR_FAIL(ctx, rtl::build_lbvh_gpu(in, out, L.scratch.p, L.scratch.cap, ctx->stream));
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->binfo, rtl::lbvh_info_ptr(L.scratch.p, P), 3 * sizeof(int),
+                                        hipMemcpyDeviceToHost, ctx->stream));
     }
-    S.scene_lo[0] = smin.x; S.scene_lo[1] = smin.y; S.scene_lo[2] = smin.z;
-    S.scene_hi[0] = smax.x; S.scene_hi[1] = smax.y; S.scene_hi[2] = smax.z;
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    float xform_ms = 0.0f, build_ms = 0.0f;
+    HIP_OR_FAIL(ctx, hipEventElapsedTime(&xform_ms, ctx->ev0, ctx->ev_x));
+    HIP_OR_FAIL(ctx, hipEventElapsedTime(&build_ms, ctx->ev_x, ctx->ev1));
+    const volatile float *hb = ctx->h_update->box;
+    float box[7];
+    for (int i = 0; i < 7; ++i) box[i] = hb[i];
+    rtd::SceneDev &S = ctx->S;
+    ctx->info.build_ms = xform_ms;
+    if (P > 0) {
+        const volatile int *bi = ctx->h_update->binfo;
+        const int binfo[3] = {bi[0], bi[1], bi[2]};
+        ctx->info.build_ms += build_ms;
+        ctx->last_bvh_depth = wide ? binfo[2] : binfo[0];
+        const int need = wide ? 3 * (binfo[2] + 1) : binfo[0] + 1;  // as run_lbvh
+        if (need > rtd::kStackTotal) {
+            ctx->has_scene = false;
+            return fail(ctx, RT_E_SCENE, "LBVH %d-wide depth %d exceeds the traversal stack; use RT_BUILD_SAH_HOST",
+                        wide ? 4 : 2, wide ? binfo[2] : binfo[0]);
+        }
+        ctx->info.nodes = wide ? binfo[1] : std::max(1, P - 1);
+        for (int c = 0; c < 3; ++c) {
+            ctx->src.in.scene_lo[c] = box[c];
+            ctx->src.in.scene_hi[c] = box[3 + c];
+        }
+        ctx->src.in.pad_abs = box[6];
+    }
+    for (int c = 0; c < 3; ++c) {
+        S.scene_lo[c] = box[c];
+        S.scene_hi[c] = box[3 + c];
+    }
     ctx->info.total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;

@@ -45,4 +45,13 @@ struct XformArgs {
 
 hipError_t transform_meshes(const XformArgs &a, hipStream_t stream);
 
+// Scene.CalculateAABB of an animated scene on the device: the mesh AABBs in
+// order, then the fixed box of the loose triangles and spheres (rest_lo/hi,
+// from the host), with the host's Unity min/max and its absolute node padding
+// (rt_abi.cpp pad_abs_of).  Writes {lo[3], hi[3], pad_abs} to box (device,
+// read by the LBVH build) and to host_box (page-locked, read after the
+// stream's synchronisation).
+hipError_t scene_box(const rtd::MeshGate *aabbs, int mesh_count, const float rest_lo[3], const float rest_hi[3],
+                     float *box, float *host_box, hipStream_t stream);
+
 }  // namespace rtx

@@ -121,7 +121,61 @@ __global__ void k_triangles(XformArgs a) {
     n[2] = -(v.z / len);
 }
 
+// One block.  The host folds acc = umin(acc, lo_m) over the meshes in order
+// (ties keep the later operand: the sign of a zero follows the last mesh that
+// attains the minimum); on NaN-free operands — mesh AABBs are (k_aabb_parts)
+// — that fold is associative, so contiguous chunks folded per thread and the
+// chunk results then combined pairwise in order (left operand first) give
+// the same bits.
+constexpr int kBoxThreads = 256;
+__device__ __forceinline__ void box_fold(float *a, const float *b) {  // a = a (earlier) folded with b (later)
+    for (int c = 0; c < 3; ++c) {
+        a[c] = rtm::umin(a[c], b[c]);
+        a[3 + c] = rtm::umax(a[3 + c], b[3 + c]);
+    }
+}
+__global__ __launch_bounds__(kBoxThreads) void k_scene_box(const rtd::MeshGate *aabbs, int mesh_count, float rlx,
+                                                           float rly, float rlz, float rhx, float rhy, float rhz,
+                                                           float *box, float *host_box) {
+    __shared__ float part[kBoxThreads][6];
+    const int t = threadIdx.x;
+    const int per = (mesh_count + kBoxThreads - 1) / kBoxThreads;
+    const int m0 = min(mesh_count, t * per), m1 = min(mesh_count, m0 + per);
+    float v[6] = {FLT_MAX, FLT_MAX, FLT_MAX, -FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (int m = m0; m < m1; ++m) {
+        const float4 l = aabbs[m].lo, h = aabbs[m].hi;
+        const float b[6] = {l.x, l.y, l.z, h.x, h.y, h.z};
+        box_fold(v, b);
+    }
+    for (int c = 0; c < 6; ++c) part[t][c] = v[c];
+    __syncthreads();
+    for (int o = 1; o < kBoxThreads; o <<= 1) {  // ordered pairwise tree: t absorbs t + o
+        if ((t & (2 * o - 1)) == 0) box_fold(part[t], part[t + o]);
+        __syncthreads();
+    }
+    if (t != 0) return;
+    for (int c = 0; c < 6; ++c) v[c] = part[0][c];
+    const float rest[6] = {rlx, rly, rlz, rhx, rhy, rhz};
+    box_fold(v, rest);
+    float scale = 1.0f;  // pad_abs_of: 2^-13 of the largest finite coordinate magnitude, at least 1
+    for (int c = 0; c < 6; ++c)
+        if (__builtin_isfinite(v[c])) scale = scale < fabsf(v[c]) ? fabsf(v[c]) : scale;
+    for (int c = 0; c < 6; ++c) {
+        box[c] = v[c];
+        host_box[c] = v[c];
+    }
+    box[6] = scale * 0x1p-13f;
+    host_box[6] = scale * 0x1p-13f;
+}
+
 }  // namespace
+
+hipError_t scene_box(const rtd::MeshGate *aabbs, int mesh_count, const float rest_lo[3], const float rest_hi[3],
+                     float *box, float *host_box, hipStream_t stream) {
+    hipLaunchKernelGGL(k_scene_box, dim3(1), dim3(kBoxThreads), 0, stream, aabbs, mesh_count, rest_lo[0], rest_lo[1],
+                       rest_lo[2], rest_hi[0], rest_hi[1], rest_hi[2], box, host_box);
+    return hipGetLastError();
+}
 
 hipError_t transform_meshes(const XformArgs &a, hipStream_t stream) {
     if (a.mesh_count <= 0) return hipSuccess;

@@ -463,6 +463,25 @@ __global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n
     }
 }
 
+// The frame's sharded counters summed into kCounterWords words (out: the
+// context's page-locked host words), so a synchronous frame reads 128 B after
+// its stream synchronisation instead of copying all 32 KB of slots.
+__global__ __launch_bounds__(256) void fold_counters_kernel(const unsigned long long *counters,
+                                                           unsigned long long *out) {
+    static_assert(kCounterWords == 16 && kCounterSlots % 16 == 0, "16 words x 16 parts");
+    const int w = threadIdx.x & 15, part = threadIdx.x >> 4;
+    unsigned long long s = 0;
+    for (int sl = part; sl < kCounterSlots; sl += 16) s += counters[(size_t)sl * kCounterWords + w];
+    __shared__ unsigned long long acc[16][16];
+    acc[part][w] = s;
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        unsigned long long t = 0;
+        for (int p = 0; p < 16; ++p) t += acc[p][threadIdx.x];
+        out[threadIdx.x] = t;
+    }
+}
+
 // Wave-synchronous megakernel: the Whitted chain advances level by level for
 // the whole wave; rays of levels < PACKET_LEVELS (camera rays and their shadow
 // rays first of all) are traced as one packet per wave (packet.h), deeper
@@ -677,6 +696,11 @@ __global__ void iota_kernel(int *p, int n) {
 hipError_t launch_iota(int *p, int n, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_fold_counters(const unsigned long long *counters, unsigned long long *out, hipStream_t stream) {
+    hipLaunchKernelGGL(fold_counters_kernel, dim3(1), dim3(256), 0, stream, counters, out);
     return hipGetLastError();
 }
 
