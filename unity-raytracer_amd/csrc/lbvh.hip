@@ -291,21 +291,6 @@ __global__ void k_bounds(int n, const float4 *slo, const float4 *shi, const int 
     }
 }
 
-// 6a. small homogeneous subtrees (<= 4 primitives of one kind and one mesh
-// gate, contiguous in leaf order) become one multi-primitive leaf in the
-// 4-wide tree — fewer traversal steps, like the host SAH build's leaves.
-__global__ void k_small(int n, const int2 *range, const int *gate_pos, int *small) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n - 1) return;
-    const int2 r = range[i];
-    bool ok = i != 0 && r.y - r.x + 1 <= kLbvhLeaf;  // the root stays a node
-    if (ok) {
-        const int g = gate_pos[r.x];
-        for (int p = r.x + 1; p <= r.y; ++p) ok = ok && gate_pos[p] == g;
-    }
-    small[i] = ok ? 1 : 0;
-}
-
 // 6b. depth of every internal node of the 2-wide tree (climb to the root;
 // depths are small): the traversal stack bound of the 2-wide layout.
 __global__ void k_depth(int n, const int *node_parent, int *max_depth) {
@@ -341,6 +326,41 @@ struct Slots4 {
 __device__ __forceinline__ float half_area(const float lo[3], const float hi[3]) {
     const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
     return dx * dy + dy * dz + dz * dx;
+}
+
+// 6a. small homogeneous subtrees (<= 4 primitives of one kind and one mesh
+// gate, contiguous in leaf order) become one multi-primitive leaf in the
+// 4-wide tree — fewer traversal steps, like the host SAH build's leaves —
+// when the host builder's leaf rule holds for them (bvh.cpp: n primitive
+// tests cost no more than a node step plus the children's area-weighted
+// tests, here with the Karras split as the split): a wave packet tests every
+// primitive of a leaf it enters on all its lanes, so over-full leaves of
+// tiny far-apart triangles cost more than the node step they save.
+__global__ void k_small(int n, const int2 *range, const int *gate_pos, const rtd::BvhNode *nodes, int *small) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n - 1) return;
+    const int2 r = range[i];
+    const int cnt = r.y - r.x + 1;
+    bool ok = i != 0 && cnt <= kLbvhLeaf;  // the root stays a node
+    if (ok) {
+        const int g = gate_pos[r.x];
+        for (int p = r.x + 1; p <= r.y; ++p) ok = ok && gate_pos[p] == g;
+    }
+    if (ok && cnt > 1) {
+        const rtd::BvhNode nd = nodes[i];
+        float l0[3], h0[3], l1[3], h1[3], lp[3], hp[3];
+        read_slot(nd, 0, l0, h0);
+        read_slot(nd, 1, l1, h1);
+        for (int a = 0; a < 3; ++a) {
+            lp[a] = fminf(l0[a], l1[a]);
+            hp[a] = fmaxf(h0[a], h1[a]);
+        }
+        const int c0 = nd.d.x >= 0 ? range[nd.d.x].y - range[nd.d.x].x + 1 : 1;
+        const float ap = fmaxf(half_area(lp, hp), 1e-30f);
+        const float split = 1.0f + (half_area(l0, h0) * (float)c0 + half_area(l1, h1) * (float)(cnt - c0)) / ap;
+        ok = (float)cnt <= split;
+    }
+    small[i] = ok ? 1 : 0;
 }
 
 // A slot's first leaf: a left child starts where its parent does; a right
@@ -601,7 +621,8 @@ hipError_t build_lbvh_gpu(const LbvhInput &in, const LbvhOutput &out, void *scra
         if (!out.nodes4)  // the 2-wide stack bound; the 4-wide one comes from k_keep
             hipLaunchKernelGGL(k_depth, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, node_parent, depth);
         else {
-            hipLaunchKernelGGL(k_small, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, range, gate_pos, small);
+            hipLaunchKernelGGL(k_small, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, range, gate_pos, out.nodes,
+                               small);
             int4 *rec = (int4 *)(b + L.rec);
             hipLaunchKernelGGL(k_slots, dim3(blocks_for(n)), dim3(kThreads), 0, stream, n, out.nodes, small, range,
                                rec);

@@ -640,12 +640,16 @@ constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this
 constexpr int kSplit16MaxTiles = 70000;
 constexpr int kSplit16DivLarge = 4096;
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
-// rt_render's host-output pipeline: row slabs of about kSlabBytes, 3 to 8 of them (C3 at 1080p: 8
-// slabs of 4.1 MB in float RGBA, 3 of 2.8 MB in RGBA8; measured best, tools/exp/e2e_sweep.py),
-// alternating over two streams; frames under kSlabMinFrame in one piece
-constexpr size_t kSlabBytes = (size_t)4 << 20;
+// rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
+// kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
+// a 0.29 ms frame — small slabs first so the copy starts early, then slabs the render keeps ahead
+// of), else kSlabsRenderBound (RGBA8 / RGBA16F: small last slab, little copy after the render);
+// measured best of 9 / 10 weight vectors on C3 (tools/exp/e2e_weights.py, profiles/r03_e2e/).
+// Frames under kSlabMinFrame go in one piece.
+constexpr double kSlabsCopyBound[] = {1, 2, 2, 3, 3, 4};
+constexpr double kSlabsRenderBound[] = {1, 2, 2, 1};
 constexpr size_t kSlabMinFrame = (size_t)2 << 20;
-constexpr int kMaxSlabs = 16;  // RT_SLABS (tuning) range
+constexpr int kMaxSlabs = 16;  // RT_SLABS / RT_SLAB_WEIGHTS (tuning) range
 
 // Enqueues the sum of the sharded ray/test counters into ctx->h_counts (read
 // after the stream's synchronisation by read_folded).
@@ -810,8 +814,8 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
 
 int lpt_sort_now(rt_ctx *ctx, const rtd::FrameDev &F, LptSlot *ls) {
     HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
-                                             (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles, ls->scratch.p,
-                                             ls->scratch.cap, ctx->stream));
+                                             (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
+                                             ls->scratch.p, ls->scratch.cap, ctx->stream));
     ls->valid = true;
     return RT_OK;
 }
@@ -884,12 +888,34 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
     // outside the timed region, which covers device work only
     if (slabs) {
         row_bytes = (int)(out_bytes / (size_t)std::max(1, F.local_rows));
-        int nslab = out_bytes < kSlabMinFrame
-                        ? 1
-                        : std::max(3, std::min(8, (int)((out_bytes + kSlabBytes / 2) / kSlabBytes)));
-        if (const char *e = std::getenv("RT_SLABS")) nslab = std::max(1, std::min(kMaxSlabs, std::atoi(e)));  // tuning
+        double wts[kMaxSlabs];
+        for (int k = 0; k < kMaxSlabs; ++k) wts[k] = 1.0;
+        const bool copy_bound = F.out_format == rtd::kOutFloat4 || F.out_format == rtd::kOutRGB32F;
+        const double *w0 = copy_bound ? kSlabsCopyBound : kSlabsRenderBound;
+        int nslab = out_bytes < kSlabMinFrame ? 1 : copy_bound ? 6 : 4;
+        if (nslab > 1)
+            for (int k = 0; k < nslab; ++k) wts[k] = w0[k];
+        if (const char *e = std::getenv("RT_SLABS")) {  // tuning: equal slabs
+            nslab = std::max(1, std::min(kMaxSlabs, std::atoi(e)));
+            for (int k = 0; k < kMaxSlabs; ++k) wts[k] = 1.0;
+        }
+        if (const char *e = std::getenv("RT_SLAB_WEIGHTS")) {  // tuning: "1,1,2,4,8"
+            nslab = 0;
+            for (const char *q = e; *q && nslab < kMaxSlabs;) {
+                wts[nslab++] = std::max(1e-3, std::atof(q));
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+            nslab = std::max(1, nslab);
+        }
+        double cum[kMaxSlabs + 1];
+        cum[0] = 0.0;
+        for (int k = 0; k < nslab; ++k) cum[k + 1] = cum[k] + wts[k];
         // slab boundaries on whole tile rows
         const int tile_rows = (F.local_rows + F.tile_h - 1) / F.tile_h;
+        auto bound = [&](int k) {
+            return std::min(F.local_rows, (int)std::lround((double)tile_rows * cum[k] / cum[nslab]) * F.tile_h);
+        };
         if (!ctx->copy_stream) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
         while ((int)ctx->slab_done.size() < nslab) {
             hipEvent_t e;
@@ -902,8 +928,8 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         for (int k = 0; k < nslab; ++k) {
             Launch L{};
             L.stream = ctx->stream = (k & 1) ? ctx->slab_stream2 : base;
-            L.r0 = std::min(F.local_rows, (int)((long long)tile_rows * k / nslab) * F.tile_h);
-            L.r1 = std::min(F.local_rows, (int)((long long)tile_rows * (k + 1) / nslab) * F.tile_h);
+            L.r0 = bound(k);
+            L.r1 = k + 1 == nslab ? F.local_rows : bound(k + 1);
             L.F = F;
             L.F.row0 = L.r0;
             L.F.local_rows = L.r1 - L.r0;
