@@ -8,7 +8,7 @@
 //     (as the reference does) and compared byte for byte with the last copy;
 //     any change re-sends the scene source (rt_set_scene_source);
 //   * otherwise only the localToWorld matrices (rt_update_mesh_transforms,
-//     64 B per mesh) — extraction and the BVH rebuild run on the GPU.
+//     64 B per mesh) — extraction and the BVH refit run on the GPU.
 // PixelColors keeps the reference's Color[] (float RGBA, RT_FLAG_OUT default);
 // set OutputRgba8 to receive Color32[] for a Texture2D instead (4x fewer
 // bytes over PCIe).
@@ -205,7 +205,9 @@ namespace RayTracer.Native
                         LocalToWorld = _matrices[i], Material = sc.MeshMats[i],
                     };
                 }
-                if (Rt.rt_set_scene_source(_rt, ref desc, src, src.Length) != Rt.OK)
+                // the tree is built once on the host and refitted on the device
+                // every Update (rigid per-mesh motion); rebuilt when it degrades
+                if (Rt.rt_set_scene_source_ex(_rt, ref desc, src, src.Length, Rt.BuildSahRefit) != Rt.OK)
                     Debug.LogError(Rt.LastError(_rt));
             }
             finally

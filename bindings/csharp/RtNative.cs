@@ -137,7 +137,7 @@ namespace RayTracer.Native
         const string Lib = "rt_mi355";
 
         public const int OK = 0;
-        public const int BuildSahHost = 0, BuildLbvhGpu = 1, BuildLbvhGpuBvh2 = 2;
+        public const int BuildSahHost = 0, BuildLbvhGpu = 1, BuildLbvhGpuBvh2 = 2, BuildSahRefit = 3;
         public const int FlagCountTests = 1, FlagWavefront = 2, FlagPacket = 4, FlagOutRgba8 = 8, FlagOutRgba16F = 16,
                          FlagAsync = 32, FlagRowOrder = 64;
 
@@ -161,6 +161,9 @@ namespace RayTracer.Native
                                                                [Out] byte[] sphereRecords, out RtBvhExportInfo info);
         [DllImport(Lib)] public static extern int rt_set_scene_source(IntPtr ctx, ref RtSceneDesc baseScene,
                                                                      [In] RtMeshSource[] meshes, int meshCount);
+        [DllImport(Lib)] public static extern int rt_set_scene_source_ex(IntPtr ctx, ref RtSceneDesc baseScene,
+                                                                        [In] RtMeshSource[] meshes, int meshCount,
+                                                                        int build);
         [DllImport(Lib)] public static extern int rt_update_mesh_transforms(IntPtr ctx, [In] RtMatrix[] localToWorld,
                                                                            int meshCount);
         [DllImport(Lib)] public static extern int rt_render(IntPtr ctx, ref CameraData cam, ref RtImagePlane plane,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum rt_status {
@@ -274,6 +274,11 @@ int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *scene);
                                  to 4-wide nodes on the GPU: for per-frame scene rebuilds
                                  (RayTracingSetup.cs:120-128) */
 #define RT_BUILD_LBVH_GPU_BVH2 2  /* the same tree left 2-wide (comparison / diagnostics) */
+#define RT_BUILD_SAH_REFIT 3  /* rt_set_scene_source_ex only: the host SAH tree once, then every
+                                 rt_update_mesh_transforms refits it on the device (same topology and
+                                 leaf order, new boxes) and rebuilds it only when the refitted tree's
+                                 surface area has grown past 1.1x that of its last build
+                                 (then on the device: the GPU LBVH, refitted from there on) */
 
 /* rt_set_scene with a choice of BVH builder.  Results are identical for every
  * builder (the BVH only accelerates Scene.IntersectRay). */
@@ -330,6 +335,14 @@ typedef struct rt_mesh_source {
  * the device; the BVH is built on the device (RT_BUILD_LBVH_GPU).  Results
  * equal rt_set_scene with the same meshes extracted on the host. */
 int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count);
+
+/* rt_set_scene_source with a choice of per-update BVH strategy: build =
+ * RT_BUILD_LBVH_GPU (rt_set_scene_source's: a device rebuild every update) or
+ * RT_BUILD_SAH_REFIT (a host SAH build here — tens of ms for 100k triangles —
+ * then device refits; for rigid per-mesh motion, the Unity Update case).
+ * Results are identical either way. */
+int rt_set_scene_source_ex(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count,
+                           int32_t build);
 
 /* Per-frame update of a scene set by rt_set_scene_source: new
  * localToWorld matrices (mesh_count x 16 floats, rt_mesh_source layout),

@@ -170,3 +170,73 @@ def test_source_errors(gpu_ctx, rt):
     with pytest.raises(rt.RtError) as e:
         gpu_ctx.update_mesh_transforms(np.stack([np.eye(4, dtype=np.float32)] * 2))
     assert e.value.status == rt.abi.RT_E_INVALID
+
+
+# ---- RT_BUILD_SAH_REFIT (rt_set_scene_source_ex): host SAH tree once, device refits ----
+
+def test_refit_updates_equal_oracle(gpu_ctx, rt, orc):
+    """Refitted trees (same topology, new boxes and records every update)
+    render each frame like the oracle on the host-extracted scene."""
+    fr, srcs, mats = rt.scenes.instanced_hall(400, res=(96, 54), spp=1, bounces=4)
+    gpu_ctx.set_scene_source(fr.scene, srcs, build=rt.abi.RT_BUILD_SAH_REFIT)
+    assert gpu_ctx.scene_info()["build"] == rt.abi.RT_BUILD_SAH_REFIT
+    for k, t in enumerate((0.0, 0.37, 1.1, 2.5)):
+        m = mats(t)
+        if k:
+            gpu_ctx.update_mesh_transforms(m)
+        img, st = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+        ref, counts = orc.render(rt.scenes.extracted(fr, srcs, m))
+        assert float(np.max(np.abs(img - ref))) <= TOL, t
+        assert _counts(st) == (counts["primary_rays"], counts["shadow_rays"], counts["reflection_rays"]), t
+
+
+def test_refit_equals_rebuilt_frames(rt):
+    """The knot spinning about its centre (the shim's rebuild loop): a
+    refitting context and a rebuilding (LBVH) context give the same frames
+    bit for bit, frame after frame, mixed mesh and loose geometry included."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from rebuild_bench import c3_sources
+    base, srcs, mats = c3_sources(rt)
+    base = base.with_resolution(320, 180)
+    a, b = rt.Context(), rt.Context()
+    try:
+        a.set_scene_source(base.scene, srcs, build=rt.abi.RT_BUILD_SAH_REFIT)
+        b.set_scene_source(base.scene, srcs)
+        for k in range(6):
+            if k:
+                m = mats(0.3 * k)
+                a.update_mesh_transforms(m)
+                b.update_mesh_transforms(m)
+            ia, sa = a.render(base.camera, base.plane, rt.frame_params(base))
+            ib, sb = b.render(base.camera, base.plane, rt.frame_params(base))
+            assert _same(ia, ib) and _counts(sa) == _counts(sb), k
+    finally:
+        a.close()
+        b.close()
+
+
+def test_refit_large_motion_rebuilds(gpu_ctx, rt, orc):
+    """Meshes scattered far from where the tree was built (the refitted
+    tree's area explodes, so the update rebuilds it on the host) and then
+    moved again: frames still equal the oracle."""
+    fr, srcs, mats = rt.scenes.instanced_hall(200, res=(64, 36), spp=1, bounces=2)
+    gpu_ctx.set_scene_source(fr.scene, srcs, build=rt.abi.RT_BUILD_SAH_REFIT)
+    m0 = mats(0.0)
+    rng = np.random.default_rng(5)
+    for step in range(3):
+        m = m0.copy()
+        perm = rng.permutation(len(m))
+        m[:, :3, 3] = m0[perm, :3, 3]  # every box jumps to another box's place
+        gpu_ctx.update_mesh_transforms(m)
+        img, st = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+        ref, counts = orc.render(rt.scenes.extracted(fr, srcs, m))
+        assert float(np.max(np.abs(img - ref))) <= TOL, step
+        assert _counts(st) == (counts["primary_rays"], counts["shadow_rays"], counts["reflection_rays"]), step
+
+
+def test_refit_rejects_unknown_build(gpu_ctx, rt):
+    fr, srcs, _ = rt.scenes.instanced_hall(8, res=(16, 16), spp=1, bounces=1)
+    with pytest.raises(rt.RtError) as e:
+        gpu_ctx.set_scene_source(fr.scene, srcs, build=rt.abi.RT_BUILD_SAH_HOST)
+    assert e.value.status == rt.abi.RT_E_INVALID

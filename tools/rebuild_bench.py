@@ -2,7 +2,8 @@
 (RayTracingSetup.cs:171-199: UpdateScene re-extracts every SceneMesh, then
 CastPixelRays): rt_update_mesh_transforms (device extraction + GPU LBVH
 rebuild) followed by a frame, against the same frames on a static host-SAH
-scene and a static GPU-LBVH scene.
+scene and a static GPU-LBVH scene; then the same loop with the tree built once
+on the host and refitted on the device per update (RT_BUILD_SAH_REFIT).
 
   python tools/rebuild_bench.py --config C3 --frames 40
 C3: the torus-knot mesh as one SceneMesh spinning slowly about y; C5i: the
@@ -82,6 +83,12 @@ def main():
     info = ctx.scene_info()
     res["rebuild_update_ms"] = round(info["total_ms"], 4)
     res["rebuild_gpu_build_ms"] = round(info["build_ms"], 4)
+    # RT_BUILD_SAH_REFIT (the C# shim's choice): host SAH tree once, refitted on the device every update
+    ctx.set_scene_source(base.scene, srcs, build=rt.abi.RT_BUILD_SAH_REFIT)
+    res["refit_kernel_ms"], res["refit_wall_ms"] = frames(True)
+    info = ctx.scene_info()
+    res["refit_update_ms"] = round(info["total_ms"], 4)
+    res["refit_gpu_ms"] = round(info["build_ms"], 4)
     res["lbvh_gap"] = round(res["static_lbvh_kernel_ms"] / res["static_sah_kernel_ms"] - 1.0, 4)
     print(json.dumps(res), flush=True)
     ctx.close()

@@ -13,7 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "librt_mi355.so")
 
-RT_ABI_VERSION = 4
+RT_ABI_VERSION = 5
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -34,6 +34,7 @@ RT_FLAG_ROW_ORDER = 64
 RT_BUILD_SAH_HOST = 0
 RT_BUILD_LBVH_GPU = 1
 RT_BUILD_LBVH_GPU_BVH2 = 2
+RT_BUILD_SAH_REFIT = 3  # rt_set_scene_source_ex: host SAH once, device refits per update
 RT_GATHER_NONE = 0
 RT_GATHER_PEER_COPY = 1
 RT_GATHER_RCCL = 2
@@ -211,6 +212,7 @@ SIGNATURES = {
     "rt_get_scene_info": (C.c_int, [_P, C.POINTER(rt_scene_info)]),
     "rt_export_bvh": (C.c_int, [_P, _P, _P, _P, C.POINTER(rt_bvh_export_info)]),
     "rt_set_scene_source": (C.c_int, [_P, C.POINTER(rt_scene_desc), _P, C.c_int32]),
+    "rt_set_scene_source_ex": (C.c_int, [_P, C.POINTER(rt_scene_desc), _P, C.c_int32, C.c_int32]),
     "rt_update_mesh_transforms": (C.c_int, [_P, _P, C.c_int32]),
     "rt_render": (C.c_int, [_P, C.POINTER(rt_camera), C.POINTER(rt_image_plane),
                             C.POINTER(rt_render_params), _P, C.POINTER(rt_stats)]),

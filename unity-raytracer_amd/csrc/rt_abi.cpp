@@ -86,13 +86,65 @@ struct LptSlot {
 };
 constexpr int kLptSlots = 16;  // streams x row slabs
 
+// Host copy of rt_set_scene_source's base scene (the caller's arrays are not
+// kept): a refitted scene's full rebuild needs it.
+struct BaseCopy {
+    std::vector<rt_triangle> tris;
+    std::vector<rt_float3> normals;
+    std::vector<rt_material> tri_mats, sph_mats;
+    std::vector<rt_sphere> sphs;
+    std::vector<rt_point_light> lights;
+    rt_scene_desc desc{};
+    void set(const rt_scene_desc &b) {
+        auto cp = [](auto &v, const auto *p, int n) { v.assign(p, p + (p ? std::max(0, n) : 0)); };
+        cp(tris, b.triangles, b.triangle_count);
+        cp(normals, b.triangle_normals, b.triangle_count);
+        cp(tri_mats, b.triangle_materials, b.triangle_count);
+        cp(sphs, b.spheres, b.sphere_count);
+        cp(sph_mats, b.sphere_materials, b.sphere_count);
+        cp(lights, b.point_lights, b.point_light_count);
+        desc = b;
+        desc.triangles = tris.data();
+        desc.triangle_normals = normals.data();
+        desc.triangle_materials = tri_mats.data();
+        desc.spheres = sphs.data();
+        desc.sphere_materials = sph_mats.data();
+        desc.point_lights = lights.data();
+    }
+};
+
+// RT_BUILD_SAH_REFIT: the host SAH tree's topology kept across updates and
+// refitted on the device (scene_xform.hip refit_tree).
+// full rebuild once the tree's relative surface area grows past this: 1.05 / 1.1 / 1.25 / never gave C3
+// 0.470 / 0.465 / 0.475 / 0.472 ms and C5i 1.048 / 1.028 / 1.037 / 1.320 ms per update + frame
+// (tools/exp/refit_sweep.sh, profiles/r03_rebuild/refit_sweep.txt)
+constexpr float kRefitRebuild = 1.1f;
+struct RefitState {
+    GrowBuf parent_slot, internal_children, arrivals, prim_lo, prim_hi, quality, rank_first, geom_first, loose;
+    int nnodes = 0, ntri = 0, nsph = 0;
+    float area_built = 0.0f;    // internal slots' half areas / the root's, after the last full build
+    int rebuilds = 0;           // full rebuilds after the first (degraded refits)
+    std::vector<rt_mesh> meshes;  // first triangle, count, material; AABBs of the last full build
+    BaseCopy base;
+    void release() {
+        for (GrowBuf *b : {&parent_slot, &internal_children, &arrivals, &prim_lo, &prim_hi, &quality, &rank_first,
+                           &geom_first, &loose}) {
+            if (b->p) (void)hipFree(b->p);
+            b->p = nullptr;
+            b->cap = 0;
+        }
+    }
+};
+
 // State kept by rt_set_scene_source for rt_update_mesh_transforms.
 struct SourceState {
     bool active = false;
+    int build = RT_BUILD_LBVH_GPU;  // or RT_BUILD_SAH_REFIT
     int mesh_count = 0, vertex_total = 0, tri_total = 0, part_total = 0;
     float rest_lo[3], rest_hi[3];  // Scene.CalculateAABB over loose triangles and spheres
     rtl::LbvhInput in{};           // device inputs of the last build
     bool wide = true;
+    RefitState refit;
 };
 
 struct DeviceArrays {
@@ -268,6 +320,7 @@ struct rt_ctx {
     struct UpdateHost {
         float box[8];  // lo[3], hi[3], pad_abs
         int binfo[4];  // lbvh_info_ptr: 2-wide depth, 4-wide nodes, 4-wide depth
+        float quality[2];  // refit: internal slots' half areas, the root's
     } *h_update = nullptr;
     hipEvent_t ev_x = nullptr;  // end of the device extraction in an update
     float *d_rays = nullptr;
@@ -1255,6 +1308,7 @@ void destroy_one(rt_ctx *ctx) {
     free_scene(ctx);
     free_wavefront(ctx);
     ctx->lb.release();
+    ctx->src.refit.release();
     for (LptSlot &l : ctx->lpt) l.release();
     if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
@@ -2004,10 +2058,114 @@ extern "C" {
 
 namespace {
 
+// ---- RT_BUILD_SAH_REFIT ------------------------------------------------
+
+rtx::RefitArgs refit_args(rt_ctx *ctx) {
+    RefitState &R = ctx->src.refit;
+    LbvhBufs &B = ctx->lb;
+    rtx::RefitArgs a{};
+    a.ntri = R.ntri;
+    a.nsph = R.nsph;
+    a.nnodes = R.nnodes;
+    a.tris = (rtd::TriRec *)ctx->S.tris;  // the host build's arrays or the LBVH's (B.*)
+    a.sphs = ctx->S.sphs;
+    a.shade = (float4 *)ctx->S.shade;
+    a.mt = ctx->mesh_tri_ranks;
+    a.ns = ctx->sphere_count;
+    a.mesh_count = ctx->src.mesh_count;
+    a.mesh_rank_first = (const int *)R.rank_first.p;
+    a.mesh_geom_first = (const int *)R.geom_first.p;
+    a.mesh_tris = (const float *)B.mesh_tris.p;
+    a.mesh_normals = (const float *)B.mesh_normals.p;
+    a.loose_tris = (const float *)R.loose.p;
+    a.box = (const float *)B.scene_box.p;
+    a.prim_lo = (float4 *)R.prim_lo.p;
+    a.prim_hi = (float4 *)R.prim_hi.p;
+    a.nodes = (rtd::BvhNode4 *)ctx->S.nodes4;
+    a.parent_slot = (const int *)R.parent_slot.p;
+    a.internal_children = (const int *)R.internal_children.p;
+    a.arrivals = (int *)R.arrivals.p;
+    a.empty_ref = rtd::encode_leaf(R.ntri, 1, rtd::kLeafTri);  // the sentinel record (both builders)
+    a.quality = (float *)R.quality.p;
+    return a;
+}
+
+// A full build of the current device geometry (world triangles as
+// extracted, exact mesh AABBs `aabbs`): the host SAH tree (rt_set_scene_source_ex)
+// or, when a refitted tree has degraded, the device LBVH (a host rebuild of a
+// big scene would stall the Update for tens of ms); then the tree's refit
+// tables and one refit of that same geometry for its reference surface area.
+int refit_build(rt_ctx *ctx, const std::vector<rtd::MeshGate> &aabbs, bool host_sah,
+                std::chrono::steady_clock::time_point t0) {
+    RefitState &R = ctx->src.refit;
+    LbvhBufs &B = ctx->lb;
+    const int tt = ctx->src.tri_total, M = ctx->src.mesh_count;
+    std::vector<rt_triangle> mtris;
+    std::vector<rt_float3> mnorm;
+    if (host_sah && tt) {
+        mtris.resize((size_t)tt);
+        mnorm.resize((size_t)tt);
+        HIP_OR_FAIL(ctx, hipMemcpy(mtris.data(), B.mesh_tris.p, sizeof(rt_triangle) * (size_t)tt, hipMemcpyDeviceToHost));
+        HIP_OR_FAIL(ctx, hipMemcpy(mnorm.data(), B.mesh_normals.p, sizeof(rt_float3) * (size_t)tt,
+                                   hipMemcpyDeviceToHost));
+    }
+    for (int m = 0; m < M; ++m) {
+        R.meshes[m].aabb.min = {aabbs[m].lo.x, aabbs[m].lo.y, aabbs[m].lo.z};
+        R.meshes[m].aabb.max = {aabbs[m].hi.x, aabbs[m].hi.y, aabbs[m].hi.z};
+    }
+    rt_scene_desc d = R.base.desc;
+    d.meshes = R.meshes.data();
+    d.mesh_count = M;
+    d.mesh_triangles = host_sah ? mtris.data() : nullptr;
+    d.mesh_triangle_normals = host_sah ? mnorm.data() : nullptr;
+    d.mesh_triangle_total = tt;
+    int st = set_scene_impl(ctx, &d, host_sah ? RT_BUILD_SAH_HOST : RT_BUILD_LBVH_GPU, !host_sah, t0);
+    if (st) return st;
+    ctx->info.build = RT_BUILD_SAH_REFIT;
+    R.nnodes = ctx->info.nodes;
+    R.ntri = ctx->mesh_tri_ranks + ctx->loose_count;
+    R.nsph = ctx->sphere_count;
+    if (R.nnodes <= 0) return RT_OK;
+    std::vector<int> rank_first((size_t)std::max(1, M)), geom_first((size_t)std::max(1, M));
+    for (int m = 0; m < M; ++m) {
+        rank_first[m] = ctx->mesh_rank_first[m];
+        geom_first[m] = R.meshes[m].first_triangle;
+    }
+    const std::vector<rt_triangle> &lt = R.base.tris;
+    HIP_OR_FAIL(ctx, ensure(ctx, R.parent_slot, sizeof(int) * (size_t)R.nnodes));
+    HIP_OR_FAIL(ctx, ensure(ctx, R.internal_children, sizeof(int) * (size_t)R.nnodes));
+    HIP_OR_FAIL(ctx, put(ctx, R.rank_first, rank_first.data(), rank_first.size()));
+    HIP_OR_FAIL(ctx, put(ctx, R.geom_first, geom_first.data(), geom_first.size()));
+    if (!lt.empty()) HIP_OR_FAIL(ctx, put(ctx, R.loose, lt.data(), lt.size()));
+    HIP_OR_FAIL(ctx, ensure(ctx, R.arrivals, sizeof(int) * (size_t)R.nnodes));
+    HIP_OR_FAIL(ctx, ensure(ctx, R.prim_lo, sizeof(float4) * (size_t)std::max(1, R.ntri + R.nsph)));
+    HIP_OR_FAIL(ctx, ensure(ctx, R.prim_hi, sizeof(float4) * (size_t)std::max(1, R.ntri + R.nsph)));
+    HIP_OR_FAIL(ctx, ensure(ctx, R.quality, 2 * sizeof(float)));
+    // the reference area: a refit of the geometry just built (the scene box
+    // and padding as an update computes them)
+    HIP_OR_FAIL(ctx, ensure(ctx, B.scene_box, 8 * sizeof(float)));
+    if (!ctx->h_update)
+        HIP_OR_FAIL(ctx, hipHostMalloc((void **)&ctx->h_update, sizeof *ctx->h_update, hipHostMallocCoherent));
+    HIP_OR_FAIL(ctx, rtx::scene_box((const rtd::MeshGate *)B.src_aabbs.p, M, ctx->src.rest_lo, ctx->src.rest_hi,
+                                    (float *)B.scene_box.p, ctx->h_update->box, ctx->stream));
+    const rtx::RefitArgs a = refit_args(ctx);
+    HIP_OR_FAIL(ctx, rtx::refit_links(a, (int *)R.parent_slot.p, (int *)R.internal_children.p, ctx->stream));
+    HIP_OR_FAIL(ctx, rtx::refit_tree(a, ctx->stream));
+    HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->quality, a.quality, 2 * sizeof(float), hipMemcpyDeviceToHost,
+                                    ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    const volatile float *q = ctx->h_update->quality;
+    R.area_built = q[1] > 0.0f ? q[0] / q[1] : 0.0f;
+    return RT_OK;
+}
+
 int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count,
-                         std::chrono::steady_clock::time_point t0) {
+                         int32_t build, std::chrono::steady_clock::time_point t0) {
     ctx->src.active = false;
     if (!base) return fail(ctx, RT_E_INVALID, "base scene is null");
+    if (build != RT_BUILD_LBVH_GPU && build != RT_BUILD_SAH_REFIT)
+        return fail(ctx, RT_E_INVALID, "rt_set_scene_source_ex: build %d is neither RT_BUILD_LBVH_GPU nor "
+                    "RT_BUILD_SAH_REFIT", build);
     if (mesh_count < 0 || (mesh_count && !meshes)) return fail(ctx, RT_E_INVALID, "bad mesh source array");
     if (base->mesh_count || base->mesh_triangle_total)
         return fail(ctx, RT_E_INVALID, "the base scene of rt_set_scene_source must not carry meshes");
@@ -2074,6 +2232,23 @@ int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_s
         dm[m].aabb.min = {aabbs[m].lo.x, aabbs[m].lo.y, aabbs[m].lo.z};
         dm[m].aabb.max = {aabbs[m].hi.x, aabbs[m].hi.y, aabbs[m].hi.z};
     }
+    rt_scene_desc rest = *base;  // loose triangles and spheres only
+    rtm::f3 lo, hi;
+    scene_aabb(&rest, lo, hi);
+    ctx->src.rest_lo[0] = lo.x; ctx->src.rest_lo[1] = lo.y; ctx->src.rest_lo[2] = lo.z;
+    ctx->src.rest_hi[0] = hi.x; ctx->src.rest_hi[1] = hi.y; ctx->src.rest_hi[2] = hi.z;
+    ctx->src.build = build;
+    if (build == RT_BUILD_SAH_REFIT) {
+        RefitState &R = ctx->src.refit;
+        R.base.set(*base);
+        R.meshes = dm;
+        R.rebuilds = 0;
+        st = refit_build(ctx, aabbs, true, t0);
+        if (st) return st;
+        ctx->info.build_ms += xform_ms;
+        ctx->src.active = true;
+        return RT_OK;
+    }
     rt_scene_desc d = *base;
     d.meshes = dm.data();
     d.mesh_count = mesh_count;
@@ -2083,12 +2258,58 @@ int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_s
     st = set_scene_impl(ctx, &d, RT_BUILD_LBVH_GPU, true, t0);
     if (st) return st;
     ctx->info.build_ms += xform_ms;
-    rt_scene_desc rest = *base;  // loose triangles and spheres only
-    rtm::f3 lo, hi;
-    scene_aabb(&rest, lo, hi);
-    ctx->src.rest_lo[0] = lo.x; ctx->src.rest_lo[1] = lo.y; ctx->src.rest_lo[2] = lo.z;
-    ctx->src.rest_hi[0] = hi.x; ctx->src.rest_hi[1] = hi.y; ctx->src.rest_hi[2] = hi.z;
     ctx->src.active = true;
+    return RT_OK;
+}
+
+// Refit half of an update (RT_BUILD_SAH_REFIT), after the extraction, the
+// scene box and the gates are enqueued: the tree refitted on the device, one
+// synchronisation; a full host rebuild when the refitted tree's relative
+// surface area has grown past kRefitRebuild x that of its last build (or is
+// not finite).
+int refit_update(rt_ctx *ctx, std::chrono::steady_clock::time_point t0) {
+    RefitState &R = ctx->src.refit;
+    const rtx::RefitArgs a = refit_args(ctx);
+    HIP_OR_FAIL(ctx, rtx::refit_tree(a, ctx->stream));
+    if (R.nnodes > 0)
+        HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->quality, a.quality, 2 * sizeof(float), hipMemcpyDeviceToHost,
+                                        ctx->stream));
+    HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    float xform_ms = 0.0f, refit_ms = 0.0f;
+    HIP_OR_FAIL(ctx, hipEventElapsedTime(&xform_ms, ctx->ev0, ctx->ev_x));
+    HIP_OR_FAIL(ctx, hipEventElapsedTime(&refit_ms, ctx->ev_x, ctx->ev1));
+    const volatile float *hb = ctx->h_update->box;
+    rtd::SceneDev &S = ctx->S;
+    for (int c = 0; c < 3; ++c) {
+        S.scene_lo[c] = hb[c];
+        S.scene_hi[c] = hb[3 + c];
+    }
+    ctx->info.build_ms = xform_ms + refit_ms;
+    if (R.nnodes > 0) {
+        const volatile float *q = ctx->h_update->quality;
+        const float area = q[1] > 0.0f ? q[0] / q[1] : 0.0f;
+        static const float limit = [] {  // tuning override
+            const char *e = std::getenv("RT_REFIT_REBUILD");
+            return e ? (float)std::atof(e) : kRefitRebuild;
+        }();
+        if (!(area <= limit * R.area_built)) {
+            std::vector<rtd::MeshGate> aabbs((size_t)ctx->src.mesh_count);
+            if (!aabbs.empty())
+                HIP_OR_FAIL(ctx, hipMemcpy(aabbs.data(), ctx->lb.src_aabbs.p, sizeof(rtd::MeshGate) * aabbs.size(),
+                                           hipMemcpyDeviceToHost));
+            const double build_ms = ctx->info.build_ms;
+            const int st = refit_build(ctx, aabbs, false, t0);
+            if (st) {
+                ctx->has_scene = false;
+                return st;
+            }
+            ++R.rebuilds;
+            ctx->info.build_ms = build_ms;
+        }
+    }
+    ctx->info.total_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
 }
 
@@ -2124,6 +2345,7 @@ int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t
         HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->arr.gates, a.aabbs, sizeof(rtd::MeshGate) * (size_t)mesh_count,
                                         hipMemcpyDeviceToDevice, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_x, ctx->stream));
+    if (ctx->src.build == RT_BUILD_SAH_REFIT) return refit_update(ctx, t0);
     const int P = ctx->src.in.mt + ctx->src.in.ns + ctx->src.in.nl;
     LbvhBufs &L = ctx->lb;
     const bool wide = ctx->src.wide;
@@ -2181,12 +2403,17 @@ int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t
 
 extern "C" {
 
-int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count) {
+int rt_set_scene_source_ex(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count,
+                           int32_t build) {
     if (!ctx) return RT_E_INVALID;
     Range range("rt_set_scene_source");
     DeviceGuard guard;
     const auto t0 = std::chrono::steady_clock::now();
-    return for_members(ctx, [&](rt_ctx *m) { return set_scene_source_one(m, base, meshes, mesh_count, t0); });
+    return for_members(ctx, [&](rt_ctx *m) { return set_scene_source_one(m, base, meshes, mesh_count, build, t0); });
+}
+
+int rt_set_scene_source(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_source *meshes, int32_t mesh_count) {
+    return rt_set_scene_source_ex(ctx, base, meshes, mesh_count, RT_BUILD_LBVH_GPU);
 }
 
 int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t mesh_count) {

@@ -54,4 +54,40 @@ hipError_t transform_meshes(const XformArgs &a, hipStream_t stream);
 hipError_t scene_box(const rtd::MeshGate *aabbs, int mesh_count, const float rest_lo[3], const float rest_hi[3],
                      float *box, float *host_box, hipStream_t stream);
 
+// Refit of a fixed 4-wide tree after the meshes moved (rt_set_scene_source_ex
+// with RT_BUILD_SAH_REFIT): the topology and the leaf order of the host SAH
+// build are kept; every mesh triangle record (v0, v1 - v0, v2 - v0) and
+// shading normal is rewritten from the extracted world triangles, every
+// primitive's padded box recomputed with the frame's padding (the builders'
+// rule), and the node boxes rebuilt bottom-up (one thread per leaf-only node
+// climbing while it is its parent's last internal child to arrive; slots
+// handed over with write-through stores, like lbvh.hip k_bounds).  Also sums
+// the internal slots' half areas and the root's, the tree-quality measure the
+// host compares with the last full build's.
+struct RefitArgs {
+    int ntri, nsph, nnodes;         // triangle records (sentinel excluded), sphere records, 4-wide nodes
+    rtd::TriRec *tris;              // leaf order; mesh triangle records rewritten
+    const rtd::SphRec *sphs;
+    float4 *shade;                  // rank-indexed; mesh triangle normals rewritten (.w kept)
+    int mt, ns;                     // ranks: [0, mt) mesh triangles, [mt, mt + ns) spheres, then loose
+    int mesh_count;
+    const int *mesh_rank_first;     // mesh_count
+    const int *mesh_geom_first;     // mesh_count
+    const float *mesh_tris;         // geometry-indexed world triangles (9 floats)
+    const float *mesh_normals;      // geometry-indexed (3 floats)
+    const float *loose_tris;        // loose-triangle vertices (9 floats each)
+    const float *box;               // {scene lo, hi, pad_abs} (k_scene_box)
+    float4 *prim_lo, *prim_hi;      // ntri + nsph padded boxes (scratch)
+    rtd::BvhNode4 *nodes;
+    const int *parent_slot;         // per node: parent * 4 + slot, -1 for the root
+    const int *internal_children;   // per node
+    int *arrivals;                  // per node, zeroed by refit_tree
+    int empty_ref;                  // the unused slots' ref (+inf boxes, left alone)
+    float *quality;                 // [0] sum of internal slots' half areas, [1] root half area (zeroed)
+};
+
+hipError_t refit_tree(const RefitArgs &a, hipStream_t stream);
+// fills a tree's parent_slot / internal_children tables (a.nodes, a.nnodes)
+hipError_t refit_links(const RefitArgs &a, int *parent_slot, int *internal_children, hipStream_t stream);
+
 }  // namespace rtx

@@ -168,7 +168,162 @@ __global__ __launch_bounds__(kBoxThreads) void k_scene_box(const rtd::MeshGate *
     host_box[6] = scale * 0x1p-13f;
 }
 
+// ---- refit (RefitArgs) ----------------------------------------------------
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void st_wt(float *p, float v) {  // write-through (sc1), see lbvh.hip
+    __hip_atomic_store((gu32 *)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float *p) {
+    return __uint_as_float(__hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// padded triangle box, the builders' rule (rt_abi.cpp add_tri_prim, lbvh.hip k_prims)
+__device__ __forceinline__ void tri_box(const float *v, float pad_abs, float4 &lo, float4 &hi) {
+    float l[3], h[3], ext = 0.0f;
+    for (int c = 0; c < 3; ++c) {
+        l[c] = fminf(v[c], fminf(v[3 + c], v[6 + c]));
+        h[c] = fmaxf(v[c], fmaxf(v[3 + c], v[6 + c]));
+        ext = fmaxf(ext, h[c] - l[c]);
+    }
+    const float pad = pad_abs + ext * 1e-4f;
+    lo = make_float4(l[0] - pad, l[1] - pad, l[2] - pad, 0.0f);
+    hi = make_float4(h[0] + pad, h[1] + pad, h[2] + pad, 0.0f);
+}
+
+__global__ void k_refit_prims(RefitArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const float pad_abs = a.box[6];
+    if (i < a.ntri) {
+        rtd::TriRec t = a.tris[i];
+        const int rank = __float_as_int(t.p2.y);
+        const float *v;
+        if (rank < a.mt) {
+            int lo_m = 0, hi_m = a.mesh_count - 1;  // last mesh with rank_first <= rank
+            while (lo_m < hi_m) {
+                const int c = (lo_m + hi_m + 1) >> 1;
+                if (a.mesh_rank_first[c] <= rank) lo_m = c; else hi_m = c - 1;
+            }
+            const int g = a.mesh_geom_first[lo_m] + (rank - a.mesh_rank_first[lo_m]);
+            v = a.mesh_tris + 9 * (size_t)g;
+            const f3 v0 = mk(v[0], v[1], v[2]), v1 = mk(v[3], v[4], v[5]), v2 = mk(v[6], v[7], v[8]);
+            const f3 e1 = v1 - v0, e2 = v2 - v0;  // RMath.cs:34-35
+            t.p0 = make_float4(v0.x, v0.y, v0.z, e1.x);
+            t.p1 = make_float4(e1.y, e1.z, e2.x, e2.y);
+            t.p2.x = e2.z;
+            a.tris[i] = t;
+            const float *n = a.mesh_normals + 3 * (size_t)g;
+            a.shade[rank] = make_float4(n[0], n[1], n[2], a.shade[rank].w);
+        } else {
+            v = a.loose_tris + 9 * (size_t)(rank - a.mt - a.ns);
+        }
+        tri_box(v, pad_abs, a.prim_lo[i], a.prim_hi[i]);
+    } else if (i < a.ntri + a.nsph) {
+        const float4 cr = a.sphs[i - a.ntri].cr;
+        const float r = sqrtf(cr.w), pad = pad_abs + r * 1e-4f;
+        a.prim_lo[i] = make_float4(cr.x - r - pad, cr.y - r - pad, cr.z - r - pad, 0.0f);
+        a.prim_hi[i] = make_float4(cr.x + r + pad, cr.y + r + pad, cr.z + r + pad, 0.0f);
+    }
+}
+
+__device__ __forceinline__ float half_area3(float4 lo, float4 hi) {
+    const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ void k_refit_nodes(RefitArgs a) {
+    int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= a.nnodes || a.internal_children[v] != 0) return;
+    for (;;) {
+        rtd::BvhNode4 *nd = a.nodes + v;
+        const int4 ch = nd->child;
+        const int refs[4] = {ch.x, ch.y, ch.z, ch.w};
+        float4 ulo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), uhi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+        float inner_area = 0.0f;
+        float *lox = &nd->lox.x, *hix = &nd->hix.x, *loy = &nd->loy.x, *hiy = &nd->hiy.x, *loz = &nd->loz.x,
+              *hiz = &nd->hiz.x;
+        for (int k = 0; k < 4; ++k) {
+            const int ref = refs[k];
+            if (ref == a.empty_ref) continue;
+            float4 lo, hi;
+            if (ref >= 0) {  // the child's thread wrote this slot
+                lo = make_float4(ld_wt(lox + k), ld_wt(loy + k), ld_wt(loz + k), 0.0f);
+                hi = make_float4(ld_wt(hix + k), ld_wt(hiy + k), ld_wt(hiz + k), 0.0f);
+                inner_area += half_area3(lo, hi);
+            } else {
+                const int d = ~ref, first = d & ((1 << rtd::kLeafFirstBits) - 1);
+                const int count = ((d >> rtd::kLeafFirstBits) & 3) + 1, kind = (d >> (rtd::kLeafFirstBits + 2)) & 1;
+                const int base = kind == rtd::kLeafSphere ? a.ntri + first : first;
+                lo = a.prim_lo[base];
+                hi = a.prim_hi[base];
+                for (int p = 1; p < count; ++p) {
+                    const float4 l = a.prim_lo[base + p], h = a.prim_hi[base + p];
+                    lo = make_float4(fminf(lo.x, l.x), fminf(lo.y, l.y), fminf(lo.z, l.z), 0.0f);
+                    hi = make_float4(fmaxf(hi.x, h.x), fmaxf(hi.y, h.y), fmaxf(hi.z, h.z), 0.0f);
+                }
+                st_wt(lox + k, lo.x); st_wt(hix + k, hi.x);
+                st_wt(loy + k, lo.y); st_wt(hiy + k, hi.y);
+                st_wt(loz + k, lo.z); st_wt(hiz + k, hi.z);
+            }
+            ulo = make_float4(fminf(ulo.x, lo.x), fminf(ulo.y, lo.y), fminf(ulo.z, lo.z), 0.0f);
+            uhi = make_float4(fmaxf(uhi.x, hi.x), fmaxf(uhi.y, hi.y), fmaxf(uhi.z, hi.z), 0.0f);
+        }
+        if (inner_area > 0.0f) atomicAdd(a.quality, inner_area);
+        const int ps = a.parent_slot[v];
+        if (ps < 0) {
+            a.quality[1] = half_area3(ulo, uhi);
+            return;
+        }
+        const int p = ps >> 2, k = ps & 3;
+        rtd::BvhNode4 *pn = a.nodes + p;
+        st_wt(&pn->lox.x + k, ulo.x); st_wt(&pn->hix.x + k, uhi.x);
+        st_wt(&pn->loy.x + k, ulo.y); st_wt(&pn->hiy.x + k, uhi.y);
+        st_wt(&pn->loz.x + k, ulo.z); st_wt(&pn->hiz.x + k, uhi.z);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot is visible before the count
+        const int arrived = __hip_atomic_fetch_add((__attribute__((address_space(1))) int *)&a.arrivals[p], 1,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        if (arrived != a.internal_children[p]) return;  // a sibling subtree is still refitting
+        v = p;
+    }
+}
+
+// the tree's links: each node's parent slot (4 * parent + slot; the root
+// keeps the -1 of the memset) and its number of internal children
+__global__ void k_refit_links(rtd::BvhNode4 *nodes, int nnodes, int *parent_slot, int *internal_children) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nnodes) return;
+    const int4 ch = nodes[v].child;
+    const int c[4] = {ch.x, ch.y, ch.z, ch.w};
+    int n = 0;
+    for (int k = 0; k < 4; ++k)
+        if (c[k] >= 0) {
+            parent_slot[c[k]] = 4 * v + k;
+            ++n;
+        }
+    internal_children[v] = n;
+}
+
 }  // namespace
+
+hipError_t refit_links(const RefitArgs &a, int *parent_slot, int *internal_children, hipStream_t stream) {
+    if (a.nnodes <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(parent_slot, 0xff, sizeof(int) * (size_t)a.nnodes, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_refit_links, dim3((a.nnodes + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, a.nodes,
+                       a.nnodes, parent_slot, internal_children);
+    return hipGetLastError();
+}
+
+hipError_t refit_tree(const RefitArgs &a, hipStream_t stream) {
+    if (a.nnodes <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(a.arrivals, 0, sizeof(int) * (size_t)a.nnodes, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(a.quality, 0, 2 * sizeof(float), stream);
+    if (e != hipSuccess) return e;
+    const int np = a.ntri + a.nsph;
+    if (np > 0) hipLaunchKernelGGL(k_refit_prims, dim3((np + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, a);
+    hipLaunchKernelGGL(k_refit_nodes, dim3((a.nnodes + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, a);
+    return hipGetLastError();
+}
 
 hipError_t scene_box(const rtd::MeshGate *aabbs, int mesh_count, const float rest_lo[3], const float rest_hi[3],
                      float *box, float *host_box, hipStream_t stream) {

@@ -123,16 +123,21 @@ class Context:
         self._check(self.lib.rt_set_scene_ex(self.h, desc.ref(), int(build)))
         self._scene_desc = desc  # keep arrays alive for the duration of the call only; harmless
 
-    def set_scene_source(self, base: Scene, sources):
+    def set_scene_source(self, base: Scene, sources, build: Optional[int] = None):
         """Device-side mesh extraction + GPU BVH build: `base` holds loose
         triangles, spheres and lights (no meshes); `sources` are MeshSource
-        objects (local vertices, index buffer, localToWorld, material)."""
+        objects (local vertices, index buffer, localToWorld, material).
+        build: None (rt_set_scene_source: a device LBVH rebuild per update) or
+        abi.RT_BUILD_LBVH_GPU / abi.RT_BUILD_SAH_REFIT (rt_set_scene_source_ex)."""
         from .scene import MeshSourceArray
         if base.Meshes:
             raise ValueError("base scene must not carry extracted meshes")
         desc = base.to_desc()
         arr = MeshSourceArray(list(sources))
-        self._check(self.lib.rt_set_scene_source(self.h, desc.ref(), arr.ptr(), arr.count))
+        if build is None:
+            self._check(self.lib.rt_set_scene_source(self.h, desc.ref(), arr.ptr(), arr.count))
+        else:
+            self._check(self.lib.rt_set_scene_source_ex(self.h, desc.ref(), arr.ptr(), arr.count, int(build)))
         self._scene_desc = desc
 
     def update_mesh_transforms(self, local_to_world):
