@@ -28,7 +28,9 @@ using rtm::mk;
 using rtt::Counts;
 using rtt::RayCtx;
 
-constexpr int kWaveStack = rtd::kStackTotal;  // 3 entries per BVH4 level
+// 3 entries per BVH4 level, plus the cut entries a camera packet may start
+// with (cut_start: at most kCutMax - 1 waiting below the first)
+constexpr int kWaveStack = rtd::kStackTotal + rtd::kCutMax;
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
@@ -111,11 +113,116 @@ __device__ __forceinline__ void packet_leaf_tris(const rtd::SceneDev &S, const R
     }
 }
 
+// The tile of a camera packet: its pixel rectangle [x0, x0 + w) x [y0, y0 +
+// h) in image coordinates (the camera samples of every lane lie inside it).
+struct TileRect {
+    int x0, y0, w, h;
+};
+
+// Is the padded box (lo, hi) outside the half-space {p : n . (p - o) >= 0}?
+// Conservative: the corner furthest along n is tested with a relative slack
+// far above the rounding of the camera-relative dot product, and a NaN never
+// culls.
+__device__ __forceinline__ bool cut_outside(f3 n, f3 clo, f3 chi) {
+    const float cx = n.x >= 0.0f ? chi.x : clo.x, cy = n.y >= 0.0f ? chi.y : clo.y,
+                cz = n.z >= 0.0f ? chi.z : clo.z;
+    const float v = fmaf(n.x, cx, fmaf(n.y, cy, n.z * cz));
+    const float mag = fmaf(fabsf(n.x), fabsf(cx), fmaf(fabsf(n.y), fabsf(cy), fabsf(n.z) * fabsf(cz)));
+    return v < -1e-5f * mag;
+}
+
+// Stack marker of a waiting cut entry (cut_select): above every node index
+// (node counts stay below 2^kLeafFirstBits).
+constexpr int kCutMark = 0x40000000;
+
+// Where a camera packet starts (cut_select): state -1 at the root, 0 when no
+// ray of the tile can hit anything, 1 at `node` with sp - 1 entries on the
+// wave stack below `topv`.
+struct CutStart {
+    int node, sp, topv, state;
+};
+
+// Start of a camera packet below the top levels of the tree: the cut entries
+// (rtd::CutTable, one per lane) whose padded boxes the tile's frustum touches
+// are the only subtrees any of its camera rays can hit, so the packet starts
+// with them on its stack — nearest first along the tile's central ray — and
+// never visits the nodes above the cut.  Only the visiting order changes,
+// never a result.  The frustum: the four planes through the camera position
+// bounding the tile's pixels widened by one pixel on every side (FrameDev
+// cut_*): every camera ray of the tile (RayTracingSetup.cs:291-296, rounded)
+// lies at least a pixel inside them.  Writes the entries below the top two
+// into wstack.  Every lane of the wave must be active (one entry per lane).
+__device__ __forceinline__ CutStart cut_select(const rtd::SceneDev &S, const rtd::FrameDev &F, const TileRect &tr,
+                                               int *wstack) {
+    CutStart cs = {0, 0, 0, -1};
+    const rtd::CutTable *T = S.cut;
+    const int n_all = rtt::cload(&T->count);
+    if (n_all <= 0) return cs;
+    const int j = rtt::lane_id();
+    bool need = false;
+    float key = INFINITY;
+    int ref = 0;
+    if (j < n_all) {
+        const float xa = (float)(tr.x0 - 1), xb = (float)(tr.x0 + tr.w + 1);
+        const float ya = (float)(tr.y0 - 1), yb = (float)(tr.y0 + tr.h + 1);
+        const f3 o = rtt::ld3(F.cam_pos);
+        const f3 lo = mk(T->lo_x[j], T->lo_y[j], T->lo_z[j]), hi = mk(T->hi_x[j], T->hi_y[j], T->hi_z[j]);
+        ref = T->ref[j];
+        const f3 clo = lo - o, chi = hi - o;
+        const f3 ax = rtt::ld3(F.cut_ax), bx = rtt::ld3(F.cut_bx), ay = rtt::ld3(F.cut_ay), by = rtt::ld3(F.cut_by);
+        const f3 nx0 = mk(fmaf(xa, bx.x, ax.x), fmaf(xa, bx.y, ax.y), fmaf(xa, bx.z, ax.z));
+        const f3 nx1 = mk(-fmaf(xb, bx.x, ax.x), -fmaf(xb, bx.y, ax.y), -fmaf(xb, bx.z, ax.z));
+        const f3 ny0 = mk(fmaf(ya, by.x, ay.x), fmaf(ya, by.y, ay.y), fmaf(ya, by.z, ay.z));
+        const f3 ny1 = mk(-fmaf(yb, by.x, ay.x), -fmaf(yb, by.y, ay.y), -fmaf(yb, by.z, ay.z));
+        need = !(cut_outside(nx0, clo, chi) || cut_outside(nx1, clo, chi) || cut_outside(ny0, clo, chi) ||
+                 cut_outside(ny1, clo, chi));
+        if (need) {
+            // entry distance along the tile's central ray A + xc R + yc U (order only)
+            const float xc = (float)tr.x0 + 0.5f * (float)tr.w, yc = (float)tr.y0 + 0.5f * (float)tr.h;
+            const f3 A = rtt::ld3(F.cut_a), R = rtt::ld3(F.cut_r), U = rtt::ld3(F.cut_u);
+            const f3 dc = mk(fmaf(yc, U.x, fmaf(xc, R.x, A.x)), fmaf(yc, U.y, fmaf(xc, R.y, A.y)),
+                             fmaf(yc, U.z, fmaf(xc, R.z, A.z)));
+            const float ix = __builtin_amdgcn_rcpf(rtt::nudge(dc.x)), iy = __builtin_amdgcn_rcpf(rtt::nudge(dc.y)),
+                        iz = __builtin_amdgcn_rcpf(rtt::nudge(dc.z));
+            const float l0 = clo.x * ix, h0 = chi.x * ix, l1 = clo.y * iy, h1 = chi.y * iy, l2 = clo.z * iz,
+                        h2 = chi.z * iz;
+            const float tn = fmaxf(fmaxf(fminf(l0, h0), fminf(l1, h1)), fmaxf(fminf(l2, h2), 0.0f));
+            const float tf = fminf(fminf(fmaxf(l0, h0), fmaxf(l1, h1)), fmaxf(l2, h2));
+            key = tn <= tf ? tn : INFINITY;
+        }
+    }
+    const unsigned long long mask = __ballot(need);
+    if (mask == 0) {
+        cs.state = 0;
+        return cs;
+    }
+    const int n = __popcll(mask);
+    // rank among the touched entries: nearer key first, ties by lane
+    int rank = 0;
+    for (unsigned long long m = mask; m; m &= m - 1) {
+        const int i = __ffsll((long long)m) - 1;
+        const float ki = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(key), i));
+        rank += (ki < key || (ki == key && i < j)) ? 1 : 0;
+    }
+    // rank 0 is visited first, rank 1 waits on top (topv), ranks >= 2 below
+    // it far-first: wstack[n - 1 - rank].  The waiting ones go as markers
+    // (kCutMark + entry): popped, an entry is visited only when a live lane
+    // still enters its box before its closest hit so far (packet_trace).
+    if (need && rank >= 2) wstack[n - 1 - rank] = kCutMark + j;
+    cs.node = __builtin_amdgcn_readlane(ref, __ffsll((long long)__ballot(need && rank == 0)) - 1);
+    if (n > 1) cs.topv = kCutMark + __ffsll((long long)__ballot(need && rank == 1)) - 1;
+    cs.sp = n - 1;
+    cs.state = 1;
+    return cs;
+}
+
 // ANY: shadow query with predicate t*t < d2 (see traverse.h).  `part`: the
 // lane takes part.  wstack: this wave's LDS stack (kWaveStack ints).
+// cs (camera packets): the start cut_select chose (null or state -1: the root).
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCtx &r, bool part, float tlimit,
-                                             float d2, PacketLane &L, int *wstack, Counts &cnt) {
+                                             float d2, PacketLane &L, int *wstack, Counts &cnt,
+                                             const CutStart *cs = nullptr) {
     L.best_t = FLT_MAX;
     L.best_rank = -1;
     L.tcull = ANY ? tlimit : FLT_MAX;
@@ -135,6 +242,12 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
     // same value); a pop hands it over at once and refills it from LDS, so
     // the LDS read overlaps the next node fetch instead of preceding it
     int topv = 0;
+    if (cs && cs->state >= 0) {
+        if (cs->state == 0) return;
+        node = cs->node;
+        sp = cs->sp;
+        topv = cs->topv;
+    }
 #define RT_PK_PUSH(v)                               \
     do {                                            \
         if (sp > 0) wstack[sp - 1] = topv;          \
@@ -150,6 +263,26 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
     // plane-row offsets in the node (lo, hi per axis): near row first
     const int ox = uni(same_signs && mx != 0), oy = uni(same_signs && my != 0), oz = uni(same_signs && mz != 0);
     while (true) {
+        if (!ANY && node >= kCutMark) {
+            // a waiting cut entry (cut_select): visited only if a live lane's
+            // ray still enters its box before the lane's closest hit so far
+            const rtd::CutTable *T = S.cut;
+            const int e = node - kCutMark;
+            const float lx = rtt::cload(T->lo_x + e), hx = rtt::cload(T->hi_x + e), ly = rtt::cload(T->lo_y + e),
+                        hy = rtt::cload(T->hi_y + e), lz = rtt::cload(T->lo_z + e), hz = rtt::cload(T->hi_z + e);
+            const int ref = rtt::cload(T->ref + e);
+            float k = INFINITY;
+            if (L.live) k = rtt::child_key(lx, hx, ly, hy, lz, hz, r, L.tcull);
+            if (COUNT && L.live) cnt.box++;
+            if (__ballot(k != INFINITY) == 0) {
+                if (sp == 0) return;
+                --sp;
+                node = uni(topv);
+                if (sp > 0) topv = wstack[sp - 1];
+                continue;
+            }
+            node = uni(ref);
+        }
 #ifdef RT_SEG_PROFILE
         if (node >= 0) L.nodes++; else L.leaves++;
 #endif

@@ -365,6 +365,7 @@ struct rt_ctx {
     int gather = RT_GATHER_NONE;
     std::vector<ncclComm_t> comms;  // one per member (RT_GATHER_RCCL)
     GroupSlot gslots[kGroupSlots];
+    rtd::CutTable *d_cut = nullptr;  // the 4-wide tree's top-level cut (enqueue_cut), once allocated
     bool warmed = false;  // the render kernels have run once on this device (warm_up)
     unsigned count_tag = 0;  // the last render_kernel launch's wave_counts tag
 };
@@ -524,6 +525,64 @@ void sky_setup(const rtd::SceneDev &S, rtd::FrameDev &F) {
     F.sky_test = 1;
 }
 
+// The camera packets' tile frustum (FrameDev cut_*, packet.h cut_start):
+// D(x, y) = A + x R + y U; the plane through the camera spanned by D(xa, .)
+// has the normal cross(A + xa R, U) = cross(A, U) + xa cross(R, U), on the
+// side x >= xa when multiplied by sign(det[A, U, R]); likewise y with
+// cross(A + ya U, R) and sign(det[A, R, U]).  Computed in double, rounded.
+void cut_setup(const rtd::SceneDev &S, rtd::FrameDev &F) {
+    F.cut_test = 0;
+    if (!S.cut || !S.bvh4 || !S.has_prims || F.res_x <= 0 || F.res_y <= 0) return;
+    if (const char *e = std::getenv("RT_NO_CUT"))  // testing: every camera packet from the root
+        if (*e && *e != '0') return;
+    // a tile's rows must lie in one band block (contiguous image rows)
+    if (F.band_count > 1 && F.band_rows % F.tile_h != 0) return;
+    double A[3], R[3], U[3];
+    for (int a = 0; a < 3; ++a) {
+        A[a] = (double)F.top_left[a] - (double)F.cam_pos[a];
+        R[a] = (double)F.right[a] * F.hl / F.res_x;
+        U[a] = -(double)F.up[a] * F.vl / F.res_y;
+    }
+    auto cross = [](const double *p, const double *q, double *o) {
+        o[0] = p[1] * q[2] - p[2] * q[1];
+        o[1] = p[2] * q[0] - p[0] * q[2];
+        o[2] = p[0] * q[1] - p[1] * q[0];
+    };
+    double aU[3], rU[3], aR[3], uR[3];
+    cross(A, U, aU);
+    cross(R, U, rU);
+    cross(A, R, aR);
+    cross(U, R, uR);
+    const double det = aU[0] * R[0] + aU[1] * R[1] + aU[2] * R[2];  // det[A, U, R]
+    bool finite = std::isfinite(det) && det != 0.0;
+    const double sx = det > 0.0 ? 1.0 : -1.0, sy = -sx;  // det[A, R, U] = -det[A, U, R]
+    for (int a = 0; a < 3; ++a) {
+        F.cut_ax[a] = (float)(sx * aU[a]);
+        F.cut_bx[a] = (float)(sx * rU[a]);
+        F.cut_ay[a] = (float)(sy * aR[a]);
+        F.cut_by[a] = (float)(sy * uR[a]);
+        F.cut_a[a] = (float)A[a];
+        F.cut_r[a] = (float)R[a];
+        F.cut_u[a] = (float)U[a];
+        finite = finite && std::isfinite(F.cut_ax[a]) && std::isfinite(F.cut_bx[a]) && std::isfinite(F.cut_ay[a]) &&
+                 std::isfinite(F.cut_by[a]) && std::isfinite(F.cam_pos[a]);
+    }
+    F.cut_test = finite ? 1 : 0;
+}
+
+// (Re)computes the top-level cut of the current 4-wide tree on the context's
+// stream, after the kernels that built or refitted it (the caller
+// synchronises the stream before any frame can read it).
+int enqueue_cut(rt_ctx *ctx) {
+    rtd::SceneDev &S = ctx->S;
+    S.cut = nullptr;
+    if (!S.bvh4 || !S.nodes4 || !S.has_prims) return RT_OK;
+    if (!ctx->d_cut) HIP_OR_FAIL(ctx, hipMalloc((void **)&ctx->d_cut, sizeof(rtd::CutTable)));
+    HIP_OR_FAIL(ctx, rtk::launch_build_cut(S.nodes4, ctx->d_cut, ctx->stream));
+    S.cut = ctx->d_cut;
+    return RT_OK;
+}
+
 int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, const rt_render_params *prm,
                   rtd::FrameDev &F, size_t &out_bytes) {
     if (!cam || !plane || !prm) return fail(ctx, RT_E_INVALID, "null camera/plane/params");
@@ -583,6 +642,7 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.out_format = f8 ? rtd::kOutRGBA8 : (f16 ? rtd::kOutRGBA16F : (f12 ? rtd::kOutRGB32F : rtd::kOutFloat4));
     out_bytes = (size_t)F.local_rows * F.res_x * rt_pixel_bytes(prm->flags);
     sky_setup(ctx->S, F);
+    cut_setup(ctx->S, F);
     return RT_OK;
 }
 
@@ -1313,6 +1373,7 @@ void destroy_one(rt_ctx *ctx) {
     if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_cut) (void)hipFree(ctx->d_cut);
     if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
     if (ctx->h_update) (void)hipHostFree(ctx->h_update);
     if (ctx->ev_x) (void)hipEventDestroy(ctx->ev_x);
@@ -1963,6 +2024,11 @@ int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geo
     }
     HIP_OR_FAIL(ctx, upload(&ctx->arr.mats, mats));
     HIP_OR_FAIL(ctx, upload(&ctx->arr.lights, lights));
+    S.has_prims = P > 0;
+    {
+        const int st = enqueue_cut(ctx);
+        if (st) return st;
+    }
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
 
     S.leaves = nullptr;
@@ -2151,6 +2217,10 @@ int refit_build(rt_ctx *ctx, const std::vector<rtd::MeshGate> &aabbs, bool host_
     const rtx::RefitArgs a = refit_args(ctx);
     HIP_OR_FAIL(ctx, rtx::refit_links(a, (int *)R.parent_slot.p, (int *)R.internal_children.p, ctx->stream));
     HIP_OR_FAIL(ctx, rtx::refit_tree(a, ctx->stream));
+    {
+        const int st = enqueue_cut(ctx);
+        if (st) return st;
+    }
     HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->quality, a.quality, 2 * sizeof(float), hipMemcpyDeviceToHost,
                                     ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
@@ -2271,6 +2341,10 @@ int refit_update(rt_ctx *ctx, std::chrono::steady_clock::time_point t0) {
     RefitState &R = ctx->src.refit;
     const rtx::RefitArgs a = refit_args(ctx);
     HIP_OR_FAIL(ctx, rtx::refit_tree(a, ctx->stream));
+    {
+        const int st = enqueue_cut(ctx);
+        if (st) return st;
+    }
     if (R.nnodes > 0)
         HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->quality, a.quality, 2 * sizeof(float), hipMemcpyDeviceToHost,
                                         ctx->stream));
@@ -2361,6 +2435,8 @@ int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t
         HIP_OR_FAIL(ctx, rtl::build_lbvh_gpu(in, out, L.scratch.p, L.scratch.cap, ctx->stream));
         HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->binfo, rtl::lbvh_info_ptr(L.scratch.p, P), 3 * sizeof(int),
                                         hipMemcpyDeviceToHost, ctx->stream));
+        const int st = enqueue_cut(ctx);
+        if (st) return st;
     }
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));

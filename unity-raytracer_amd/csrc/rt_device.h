@@ -122,6 +122,20 @@ struct alignas(16) MeshGate {
     float4 hi;
 };
 
+// A cut of the 4-wide tree: up to kCutMax subtrees (internal nodes or leaf
+// refs) such that every leaf lies below exactly one of them, with their padded
+// boxes (SoA, one entry per lane).  A camera packet starts from the entries
+// its tile's frustum touches instead of walking the top levels node by node
+// (packet.h cut_start).  Built on the device from nodes4 after every tree
+// change (trace.hip build_cut_kernel); count 0 = no cut (start at the root).
+constexpr int kCutMax = 64;
+struct CutTable {
+    float lo_x[kCutMax], lo_y[kCutMax], lo_z[kCutMax];
+    float hi_x[kCutMax], hi_y[kCutMax], hi_z[kCutMax];
+    int ref[kCutMax];
+    int count;
+};
+
 // Everything a kernel needs to read the scene.
 struct SceneDev {
     const BvhNode *nodes;
@@ -142,6 +156,7 @@ struct SceneDev {
     float scene_hi[3];
     float ambient[3];    // AmbientLight.Radiance
     float spec_threshold;  // d < spec_threshold  <=>  degrees(acos(d)) > 90f
+    const CutTable *cut;   // bvh4 scenes: the top-level cut (null: none)
 };
 
 // Longest-first dispatch key of one tile (render_kernel): its shader-clock
@@ -213,6 +228,16 @@ struct FrameDev {
     float sky_tlc[3];        // top_left - cam_pos
     float sky_hx, sky_vy;    // HorizontalLength / res_x, VerticalLength / res_y
     float sky_lo[3], sky_hi[3];  // padded Scene.AABB - cam_pos
+    // Tile frustum of the camera packets (packet.h cut_start): the camera ray
+    // of image point (x, y) (pixel units, y down) runs along D(x, y) = A + x R
+    // + y U with A = TopLeft - Position, R = right * hl / res_x, U = -up * vl /
+    // res_y (RayTracingSetup.cs:291-296).  The plane through Position bounding
+    // the tile on the side x >= xa has the normal cut_ax + xa * cut_bx (the
+    // side x <= xb: its negation at xb), likewise y with cut_ay / cut_by;
+    // signs make the tile's side positive.  cut_test 0: start at the root.
+    int cut_test;
+    float cut_ax[3], cut_bx[3], cut_ay[3], cut_by[3];
+    float cut_a[3], cut_r[3], cut_u[3];  // A, R, U (the central ray's direction orders the entries)
 };
 
 }  // namespace rtd

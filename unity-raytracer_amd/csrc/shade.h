@@ -8,6 +8,7 @@
 
 #include "rt_device.h"
 #include "rt_math.h"
+#include "packet.h"
 #include "traverse.h"
 
 namespace rts {
@@ -214,6 +215,22 @@ __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, 
     } else {
         ((float4 *)F.out)[idx] = make_float4(r, g, b, 1.0f);
     }
+}
+
+// The pixel rectangle of a tile (image rows; tile index wave-uniform) for the
+// camera packet's frustum start (packet.h cut_start).  Valid when a tile's
+// rows lie in one band block (rt_abi.cpp cut_setup checks band_rows).
+template <bool Q4 = false>
+__device__ __forceinline__ rtp::TileRect tile_rect(const rtd::FrameDev &F, int tile) {
+    const int tw = Q4 ? 4 : F.tile_w, th = Q4 ? 4 : F.tile_h;
+    const int ty = tile / F.tiles_x, tx = tile - ty * F.tiles_x;
+    const int ly = ty * th;
+    int gy = ly + F.row0;
+    if (F.band_count > 1) {
+        const int blk = ly / F.band_rows;
+        gy = (blk * F.band_count + F.band_index) * F.band_rows + (ly - blk * F.band_rows);
+    }
+    return rtp::TileRect{tx * tw, gy, tw, th};
 }
 
 // Slot (tile, lane) -> pixel; false for lanes outside the image/shard.  A

@@ -213,14 +213,14 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 // The counting launch keeps the per-ray traversal's canonical counts.
 template <bool COUNT, bool DEEP>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
-                                         int *wstack, Counts &cnt, SegClock &sg) {
+                                         int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs) {
     (void)sg;
     if (COUNT || !S.bvh4) return shade_levels<COUNT, DEEP>(S, F, o, d, 0, st, cnt);
     RT_SEG(const unsigned long long tq0 = __builtin_amdgcn_s_memtime();)
     rtt::RayCtx r;
     rtt::setup_ray(r, o, d);
     rtp::PacketLane P;
-    rtp::packet_trace<false, COUNT>(S, r, true, 0.0f, 0.0f, P, wstack, cnt);
+    rtp::packet_trace<false, COUNT>(S, r, true, 0.0f, 0.0f, P, wstack, cnt, &cs);
     RT_SEG(sg.visits += P.nodes + ((unsigned long long)P.leaves << 32);
            const unsigned long long tq1 = __builtin_amdgcn_s_memtime(); sg.setup = tq0; sg.prim = tq1 - tq0;)
     if (P.best_rank < 0) return rtt::ld3(F.bg255);  // :310-311
@@ -282,6 +282,9 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
 #ifndef RT_EXP_NOSKY
     if (!COUNT) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4>(F, px, gy, s))) == 0;
 #endif
+    // the camera packet's start below the top-level cut (every lane active here)
+    rtp::CutStart cs = {0, 0, 0, -1};
+    if (!COUNT && !sky && F.cut_test) cs = rtp::cut_select(S, F, rts::tile_rect<Q4>(F, tile), wstack);
     if (active) {
         if (COUNT) cnt.primary += 1;  // otherwise F.primary_total, added once per launch
         if (sky) {
@@ -295,7 +298,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
                 cnt.scene_miss +=
                     !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
             }
-            color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg);
+            color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg, cs);
         }
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
@@ -626,9 +629,67 @@ __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int ba
     image[i] = gathered[((size_t)band * local_rows + ly) * res_x + x];
 }
 
+// The top-level cut of a 4-wide tree (rtd::CutTable): starting from the
+// root's children, the internal entry with the largest box surface is
+// replaced by its children while the cut has room for them.  One thread; a
+// few microseconds after each tree build or refit.
+__global__ void build_cut_kernel(const BvhNode4 *nodes, CutTable *out) {
+    if (threadIdx.x != 0) return;
+    int ref[kCutMax];
+    float lo[kCutMax][3], hi[kCutMax][3], area[kCutMax];
+    int n = 0;
+    // the children of `node` in place of entry `at` (the first) and appended
+    auto expand = [&](int node, int at) {
+        const BvhNode4 nd = nodes[node];
+        const float lx[4] = {nd.lox.x, nd.lox.y, nd.lox.z, nd.lox.w}, hx[4] = {nd.hix.x, nd.hix.y, nd.hix.z, nd.hix.w};
+        const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w}, hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
+        const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w}, hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
+        const int ch[4] = {nd.child.x, nd.child.y, nd.child.z, nd.child.w};
+        for (int c = 0; c < 4; ++c) {
+            if (lx[c] == INFINITY && hx[c] == INFINITY) continue;  // empty slot
+            const int k = at >= 0 ? at : n++;
+            at = -1;
+            ref[k] = ch[c];
+            lo[k][0] = lx[c]; lo[k][1] = ly[c]; lo[k][2] = lz[c];
+            hi[k][0] = hx[c]; hi[k][1] = hy[c]; hi[k][2] = hz[c];
+            const float ex = hx[c] - lx[c], ey = hy[c] - ly[c], ez = hz[c] - lz[c];
+            area[k] = ch[c] >= 0 ? ex * ey + ey * ez + ez * ex : -1.0f;  // leaves never expand
+            if (!(area[k] >= 0.0f) && ch[c] >= 0) area[k] = 0.0f;  // NaN box: expandable last
+        }
+    };
+    expand(0, -1);
+    while (true) {
+        int best = -1;
+        for (int i = 0; i < n; ++i)
+            if (area[i] >= 0.0f && (best < 0 || area[i] > area[best])) best = i;
+        if (best < 0) break;
+        const BvhNode4 nd = nodes[ref[best]];
+        const int c = (nd.lox.x == INFINITY && nd.hix.x == INFINITY ? 0 : 1) +
+                      (nd.lox.y == INFINITY && nd.hix.y == INFINITY ? 0 : 1) +
+                      (nd.lox.z == INFINITY && nd.hix.z == INFINITY ? 0 : 1) +
+                      (nd.lox.w == INFINITY && nd.hix.w == INFINITY ? 0 : 1);
+        if (c == 0 || n - 1 + c > kCutMax) {
+            area[best] = -1.0f;  // stays in the cut as it is
+            continue;
+        }
+        expand(ref[best], best);
+    }
+    for (int i = 0; i < n; ++i) {
+        out->lo_x[i] = lo[i][0]; out->lo_y[i] = lo[i][1]; out->lo_z[i] = lo[i][2];
+        out->hi_x[i] = hi[i][0]; out->hi_y[i] = hi[i][1]; out->hi_z[i] = hi[i][2];
+        out->ref[i] = ref[i];
+    }
+    out->count = n;
+}
+
 }  // namespace
 
 namespace rtk {
+
+hipError_t launch_build_cut(const BvhNode4 *nodes, CutTable *out, hipStream_t stream) {
+    hipLaunchKernelGGL(build_cut_kernel, dim3(1), dim3(64), 0, stream, nodes, out);
+    return hipGetLastError();
+}
 
 // all-packet levels pay off where a wave's tile is small on screen (its
 // mirror rays stay coherent): 16+ samples per pixel = at most 2x2 pixels

@@ -38,7 +38,11 @@ constexpr int kLvWavesHighSpp = 7;
 // traversal the kernel needs no LDS lane stack and 72-80 VGPRs (7 or 6
 // waves/SIMD, kLvWaves*); the mirror fold (c + km*(...), evaluated back to front as the
 // recursion rounds) lives in scratch and is touched only by mirror lanes.
-// Same arithmetic per sample as render_kernel.
+// Same arithmetic per sample as render_kernel.  The camera packets start at
+// the root: the top-level cut start (packet.h cut_select) measured +5 % on C4
+// and +15 % on C5 here (per-wave selection cost on 1- and 4-pixel tiles, more
+// spills in the level loop; round 3, tools/exp/ab_cfg.sh).
+
 template <int MIN_WAVES>
 __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
