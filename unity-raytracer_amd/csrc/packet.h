@@ -266,13 +266,10 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
         if (!ANY && node >= kCutMark) {
             // a waiting cut entry (cut_select): visited only if a live lane's
             // ray still enters its box before the lane's closest hit so far
-            const rtd::CutTable *T = S.cut;
-            const int e = node - kCutMark;
-            const float lx = rtt::cload(T->lo_x + e), hx = rtt::cload(T->hi_x + e), ly = rtt::cload(T->lo_y + e),
-                        hy = rtt::cload(T->hi_y + e), lz = rtt::cload(T->lo_z + e), hz = rtt::cload(T->hi_z + e);
-            const int ref = rtt::cload(T->ref + e);
+            const rtd::CutBox b = rtt::cload(S.cut->box + (node - kCutMark));
+            const int ref = __float_as_int(b.lo.w);
             float k = INFINITY;
-            if (L.live) k = rtt::child_key(lx, hx, ly, hy, lz, hz, r, L.tcull);
+            if (L.live) k = rtt::child_key(b.lo.x, b.hi.x, b.lo.y, b.hi.y, b.lo.z, b.hi.z, r, L.tcull);
             if (COUNT && L.live) cnt.box++;
             if (__ballot(k != INFINITY) == 0) {
                 if (sp == 0) return;

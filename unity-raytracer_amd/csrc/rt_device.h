@@ -129,11 +129,17 @@ struct alignas(16) MeshGate {
 // (packet.h cut_start).  Built on the device from nodes4 after every tree
 // change (trace.hip build_cut_kernel); count 0 = no cut (start at the root).
 constexpr int kCutMax = 64;
+struct CutBox {  // one entry whole (32 B): the popped-marker test's scalar loads
+    float4 lo;     // lo.xyz, ref (bits)
+    float4 hi;     // hi.xyz, -
+};
 struct CutTable {
     float lo_x[kCutMax], lo_y[kCutMax], lo_z[kCutMax];
     float hi_x[kCutMax], hi_y[kCutMax], hi_z[kCutMax];
     int ref[kCutMax];
     int count;
+    int pad[3];
+    CutBox box[kCutMax];
 };
 
 // Everything a kernel needs to read the scene.

@@ -678,6 +678,8 @@ __global__ void build_cut_kernel(const BvhNode4 *nodes, CutTable *out) {
         out->lo_x[i] = lo[i][0]; out->lo_y[i] = lo[i][1]; out->lo_z[i] = lo[i][2];
         out->hi_x[i] = hi[i][0]; out->hi_y[i] = hi[i][1]; out->hi_z[i] = hi[i][2];
         out->ref[i] = ref[i];
+        out->box[i].lo = make_float4(lo[i][0], lo[i][1], lo[i][2], __int_as_float(ref[i]));
+        out->box[i].hi = make_float4(hi[i][0], hi[i][1], hi[i][2], 0.0f);
     }
     out->count = n;
 }
