@@ -703,7 +703,12 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     FrameDev F = F0;
     F.primary_total = active_samples(F.res_x, F.res_y, F.local_rows, F.row0, F.band_index, F.band_count, F.band_rows,
                                      F.spp);
-    const int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
+    int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
+#ifdef RT_EXP_DROP_TAIL
+    // measurement only: the last N waves of the longest-first order (the sky
+    // tiles) are not launched (their pixels are left as they were)
+    if (const char *e = getenv("RT_EXP_DROP_TAIL")) blocks = blocks > atoi(e) ? blocks - atoi(e) : 0;
+#endif
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)

@@ -64,10 +64,19 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     {
         int px, ly, gy, s;
         alive = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
+        // a wave whose samples all surely miss the padded Scene.AABB is
+        // background without its exact rays (shade.h sky_maybe, as render_kernel)
+        // (the <= 16-spp instance: C4 -8 %; at 64 spp, 1-pixel tiles, +1 %)
+        const bool sky = MIN_WAVES == kLvWavesLowSpp &&
+                         __ballot(alive && (!F.sky_test || rts::sky_maybe(F, px, gy, s))) == 0;
         if (alive) {
-            rts::primary_ray(F, px, gy, s, o, d);
             if (!F.wave_counts) cnt.primary = 1;  // otherwise F.primary_total, once per launch
+            if (sky)
+                term = rtt::ld3(F.bg255);  // :310-311
+            else
+                rts::primary_ray(F, px, gy, s, o, d);
         }
+        if (sky) alive = false;
     }
     for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
         rtt::RayCtx r;
