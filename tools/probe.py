@@ -21,7 +21,7 @@ def seg_per_wave(st):
     v = st.box_tests
     return {"waves": w, "nodes": round((v & 0xffffffff) / w, 2), "leaves": round((v >> 32) / w, 2),
             "prim_cyc": round(st.triangle_tests / w), "shadow_cyc": round(st.sphere_tests / w),
-            "total_cyc": round(st.shading_fetches / w)}
+            "total_cyc": round(st.shading_fetches / w), "setup_cyc": round(st.primary_scene_misses / w)}
 
 
 def main():

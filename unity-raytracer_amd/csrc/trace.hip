@@ -399,10 +399,11 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
             atomicMax(ctr + 6, ts1 - ts0);
 #else
             unsigned long long *ctr = F.counters + (size_t)(blockIdx.x % kCounterSlots) * kCounterWords;
-            atomicAdd(ctr + 3, vi);  // packet visits: internal | leaves << 32 (setup clock su unused)
+            atomicAdd(ctr + 3, vi);  // packet visits: internal | leaves << 32
             atomicAdd(ctr + 4, pr);
             atomicAdd(ctr + 5, sh);
             atomicAdd(ctr + 6, ts1 - ts0);
+            atomicAdd(ctr + 7, su);  // tile start -> camera packet (slot mapping, sky test, cut, primary ray)
 #endif
         }
     }
