@@ -3,7 +3,7 @@
 # trace kernel for C3 / C4 / C5 (whole frame and one rank's 1/8 band), the
 # one-rank shares at N = 2/4/8 (C3) and N = 8 (C4, C5), and the RCCL path at
 # one rank.  Every step has its own time limit; the first failure ends it.
-# usage: bash tools/r03_full.sh <tag> [notests]
+# usage: [PMCS="C3:1 C4:1"] [SIMS=0] bash tools/r03_full.sh <tag> [notests]
 set -o pipefail
 tag=${1:-cur}
 R=$GRAFT_REPO_ROOT
@@ -24,10 +24,11 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/kt_$tag -o r
   python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --streams 1 --moving-frames 0 > $R/gpurun_out/kt_$tag.log 2>&1 || { echo kt-fail; exit 1; }
 echo kt-ok
 cd $R
-for cb in C3:1 C3:8 C4:1 C4:8 C5:1 C5:8; do
+for cb in ${PMCS:-C3:1 C3:8 C4:1 C4:8 C5:1 C5:8}; do
   bash tools/pmc_round.sh $tag ${cb%%:*} ${cb##*:} > gpurun_out/pmcr_${tag}_${cb%%:*}_${cb##*:}.log 2>&1 || { echo pmc-fail-$cb; tail gpurun_out/pmcr_${tag}_${cb%%:*}_${cb##*:}.log; exit 1; }
   echo pmc-ok-$cb
 done
+[ "${SIMS:-1}" = 0 ] && { echo ALLDONE; exit 0; }
 for n in 2 4 8; do
   timeout -k 10 300 python bench.py --steps 100 --warmup 5 --no-cpu-baseline --sim-bands $n > gpurun_out/sb${n}_$tag.log 2>&1 || { echo sb$n-fail; exit 1; }
 done

@@ -631,14 +631,18 @@ __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int ba
 }
 
 // The top-level cut of a 4-wide tree (rtd::CutTable): starting from the
-// root's children, the internal entry with the largest box surface is
-// replaced by its children while the cut has room for them.  One thread; a
-// few microseconds after each tree build or refit.
-__global__ void build_cut_kernel(const BvhNode4 *nodes, CutTable *out) {
-    if (threadIdx.x != 0) return;
-    int ref[kCutMax];
-    float lo[kCutMax][3], hi[kCutMax][3], area[kCutMax];
-    int n = 0;
+// root's children, the internal entry with the largest box surface (the
+// lowest entry among equals) is replaced by its children -- the first
+// non-empty child in its place, the others appended -- while the cut has room
+// for them.  One wave, entry i in lane i: a step is one wave-wide arg-max and
+// one node fetch; every new entry fetches its own node's child count at once
+// (a few tens of microseconds after each tree build or refit; the first,
+// single-thread version spent 0.6 ms walking its arrays through scratch).
+__global__ __launch_bounds__(64) void build_cut_kernel(const BvhNode4 *nodes, CutTable *out) {
+    const int lane = threadIdx.x;
+    int ref = 0, kids = 0;  // kids: the entry's own node's non-empty children (internal entries)
+    float lo0 = 0.0f, lo1 = 0.0f, lo2 = 0.0f, hi0 = 0.0f, hi1 = 0.0f, hi2 = 0.0f, area = -1.0f;
+    int n = 0;  // wave-uniform
     // the children of `node` in place of entry `at` (the first) and appended
     auto expand = [&](int node, int at) {
         const BvhNode4 nd = nodes[node];
@@ -646,43 +650,50 @@ __global__ void build_cut_kernel(const BvhNode4 *nodes, CutTable *out) {
         const float ly[4] = {nd.loy.x, nd.loy.y, nd.loy.z, nd.loy.w}, hy[4] = {nd.hiy.x, nd.hiy.y, nd.hiy.z, nd.hiy.w};
         const float lz[4] = {nd.loz.x, nd.loz.y, nd.loz.z, nd.loz.w}, hz[4] = {nd.hiz.x, nd.hiz.y, nd.hiz.z, nd.hiz.w};
         const int ch[4] = {nd.child.x, nd.child.y, nd.child.z, nd.child.w};
+        bool mine = false;
         for (int c = 0; c < 4; ++c) {
             if (lx[c] == INFINITY && hx[c] == INFINITY) continue;  // empty slot
             const int k = at >= 0 ? at : n++;
             at = -1;
-            ref[k] = ch[c];
-            lo[k][0] = lx[c]; lo[k][1] = ly[c]; lo[k][2] = lz[c];
-            hi[k][0] = hx[c]; hi[k][1] = hy[c]; hi[k][2] = hz[c];
+            if (lane != k) continue;
+            mine = true;
+            ref = ch[c];
+            lo0 = lx[c]; lo1 = ly[c]; lo2 = lz[c];
+            hi0 = hx[c]; hi1 = hy[c]; hi2 = hz[c];
             const float ex = hx[c] - lx[c], ey = hy[c] - ly[c], ez = hz[c] - lz[c];
-            area[k] = ch[c] >= 0 ? ex * ey + ey * ez + ez * ex : -1.0f;  // leaves never expand
-            if (!(area[k] >= 0.0f) && ch[c] >= 0) area[k] = 0.0f;  // NaN box: expandable last
+            area = ch[c] >= 0 ? ex * ey + ey * ez + ez * ex : -1.0f;  // leaves never expand
+            if (!(area >= 0.0f) && ch[c] >= 0) area = 0.0f;  // NaN box: expandable last
+        }
+        if (mine && ref >= 0) {
+            const BvhNode4 own = nodes[ref];
+            kids = (own.lox.x == INFINITY && own.hix.x == INFINITY ? 0 : 1) +
+                   (own.lox.y == INFINITY && own.hix.y == INFINITY ? 0 : 1) +
+                   (own.lox.z == INFINITY && own.hix.z == INFINITY ? 0 : 1) +
+                   (own.lox.w == INFINITY && own.hix.w == INFINITY ? 0 : 1);
         }
     };
     expand(0, -1);
     while (true) {
-        int best = -1;
-        for (int i = 0; i < n; ++i)
-            if (area[i] >= 0.0f && (best < 0 || area[i] > area[best])) best = i;
-        if (best < 0) break;
-        const BvhNode4 nd = nodes[ref[best]];
-        const int c = (nd.lox.x == INFINITY && nd.hix.x == INFINITY ? 0 : 1) +
-                      (nd.lox.y == INFINITY && nd.hix.y == INFINITY ? 0 : 1) +
-                      (nd.lox.z == INFINITY && nd.hix.z == INFINITY ? 0 : 1) +
-                      (nd.lox.w == INFINITY && nd.hix.w == INFINITY ? 0 : 1);
+        float m = area;
+        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        const unsigned long long at_max = __ballot(area >= 0.0f && area == m);
+        if (!(m >= 0.0f) || at_max == 0) break;
+        const int best = __ffsll((long long)at_max) - 1;
+        const int bref = __shfl(ref, best), c = __shfl(kids, best);
         if (c == 0 || n - 1 + c > kCutMax) {
-            area[best] = -1.0f;  // stays in the cut as it is
+            if (lane == best) area = -1.0f;  // stays in the cut as it is
             continue;
         }
-        expand(ref[best], best);
+        expand(bref, best);
     }
-    for (int i = 0; i < n; ++i) {
-        out->lo_x[i] = lo[i][0]; out->lo_y[i] = lo[i][1]; out->lo_z[i] = lo[i][2];
-        out->hi_x[i] = hi[i][0]; out->hi_y[i] = hi[i][1]; out->hi_z[i] = hi[i][2];
-        out->ref[i] = ref[i];
-        out->box[i].lo = make_float4(lo[i][0], lo[i][1], lo[i][2], __int_as_float(ref[i]));
-        out->box[i].hi = make_float4(hi[i][0], hi[i][1], hi[i][2], 0.0f);
+    if (lane < n) {
+        out->lo_x[lane] = lo0; out->lo_y[lane] = lo1; out->lo_z[lane] = lo2;
+        out->hi_x[lane] = hi0; out->hi_y[lane] = hi1; out->hi_z[lane] = hi2;
+        out->ref[lane] = ref;
+        out->box[lane].lo = make_float4(lo0, lo1, lo2, __int_as_float(ref));
+        out->box[lane].hi = make_float4(hi0, hi1, hi2, 0.0f);
     }
-    out->count = n;
+    if (lane == 0) out->count = n;
 }
 
 }  // namespace
