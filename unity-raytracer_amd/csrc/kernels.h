@@ -23,6 +23,8 @@ hipError_t sort_tiles_by_cost(const unsigned *cost, unsigned *cost_sorted, const
 // The top-level cut of a 4-wide tree (rtd::CutTable), after every tree build
 // or refit, on the stream of that build.
 hipError_t launch_build_cut(const rtd::BvhNode4 *nodes, rtd::CutTable *out, hipStream_t stream);
+// the same cut with its boxes re-read from the (refitted) tree
+hipError_t launch_refresh_cut(const rtd::BvhNode4 *nodes, rtd::CutTable *out, hipStream_t stream);
 
 hipError_t launch_render_mega(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
                               hipStream_t stream);

@@ -583,6 +583,15 @@ int enqueue_cut(rt_ctx *ctx) {
     return RT_OK;
 }
 
+// After a refit of the tree the cut was built for (same topology): the same
+// subtrees with their new boxes.
+int enqueue_cut_refresh(rt_ctx *ctx) {
+    rtd::SceneDev &S = ctx->S;
+    if (!S.cut || !S.bvh4 || !S.nodes4 || !S.has_prims) return enqueue_cut(ctx);
+    HIP_OR_FAIL(ctx, rtk::launch_refresh_cut(S.nodes4, ctx->d_cut, ctx->stream));
+    return RT_OK;
+}
+
 int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, const rt_render_params *prm,
                   rtd::FrameDev &F, size_t &out_bytes) {
     if (!cam || !plane || !prm) return fail(ctx, RT_E_INVALID, "null camera/plane/params");
@@ -2342,7 +2351,7 @@ int refit_update(rt_ctx *ctx, std::chrono::steady_clock::time_point t0) {
     const rtx::RefitArgs a = refit_args(ctx);
     HIP_OR_FAIL(ctx, rtx::refit_tree(a, ctx->stream));
     {
-        const int st = enqueue_cut(ctx);
+        const int st = enqueue_cut_refresh(ctx);
         if (st) return st;
     }
     if (R.nnodes > 0)

@@ -641,6 +641,7 @@ __global__ void assemble_kernel(const Px *gathered, int res_x, int res_y, int ba
 __global__ __launch_bounds__(64) void build_cut_kernel(const BvhNode4 *nodes, CutTable *out) {
     const int lane = threadIdx.x;
     int ref = 0, kids = 0;  // kids: the entry's own node's non-empty children (internal entries)
+    int from = 0;           // the entry's parent node * 4 + child slot (refresh_cut_kernel)
     float lo0 = 0.0f, lo1 = 0.0f, lo2 = 0.0f, hi0 = 0.0f, hi1 = 0.0f, hi2 = 0.0f, area = -1.0f;
     int n = 0;  // wave-uniform
     // the children of `node` in place of entry `at` (the first) and appended
@@ -658,6 +659,7 @@ __global__ __launch_bounds__(64) void build_cut_kernel(const BvhNode4 *nodes, Cu
             if (lane != k) continue;
             mine = true;
             ref = ch[c];
+            from = node * 4 + c;
             lo0 = lx[c]; lo1 = ly[c]; lo2 = lz[c];
             hi0 = hx[c]; hi1 = hy[c]; hi2 = hz[c];
             const float ex = hx[c] - lx[c], ey = hy[c] - ly[c], ez = hz[c] - lz[c];
@@ -691,9 +693,32 @@ __global__ __launch_bounds__(64) void build_cut_kernel(const BvhNode4 *nodes, Cu
         out->hi_x[lane] = hi0; out->hi_y[lane] = hi1; out->hi_z[lane] = hi2;
         out->ref[lane] = ref;
         out->box[lane].lo = make_float4(lo0, lo1, lo2, __int_as_float(ref));
-        out->box[lane].hi = make_float4(hi0, hi1, hi2, 0.0f);
+        out->box[lane].hi = make_float4(hi0, hi1, hi2, __int_as_float(from));
     }
     if (lane == 0) out->count = n;
+}
+
+// After a refit (same topology, new boxes: rt_abi.cpp refit_update) the cut
+// keeps its subtrees and only takes their new padded boxes from their parents'
+// child slots: one fetch per entry instead of the greedy selection's chain of
+// dependent node fetches.  The subtrees still partition the leaves, so every
+// camera ray's answer is unchanged (packet.h cut_select).
+__global__ __launch_bounds__(64) void refresh_cut_kernel(const BvhNode4 *nodes, CutTable *out) {
+    const int lane = threadIdx.x;
+    if (lane >= out->count) return;
+    const int from = __float_as_int(out->box[lane].hi.w);
+    const BvhNode4 nd = nodes[from >> 2];
+    const int c = from & 3;
+    const float lo0 = c == 0 ? nd.lox.x : c == 1 ? nd.lox.y : c == 2 ? nd.lox.z : nd.lox.w;
+    const float lo1 = c == 0 ? nd.loy.x : c == 1 ? nd.loy.y : c == 2 ? nd.loy.z : nd.loy.w;
+    const float lo2 = c == 0 ? nd.loz.x : c == 1 ? nd.loz.y : c == 2 ? nd.loz.z : nd.loz.w;
+    const float hi0 = c == 0 ? nd.hix.x : c == 1 ? nd.hix.y : c == 2 ? nd.hix.z : nd.hix.w;
+    const float hi1 = c == 0 ? nd.hiy.x : c == 1 ? nd.hiy.y : c == 2 ? nd.hiy.z : nd.hiy.w;
+    const float hi2 = c == 0 ? nd.hiz.x : c == 1 ? nd.hiz.y : c == 2 ? nd.hiz.z : nd.hiz.w;
+    out->lo_x[lane] = lo0; out->lo_y[lane] = lo1; out->lo_z[lane] = lo2;
+    out->hi_x[lane] = hi0; out->hi_y[lane] = hi1; out->hi_z[lane] = hi2;
+    out->box[lane].lo = make_float4(lo0, lo1, lo2, out->box[lane].lo.w);
+    out->box[lane].hi = make_float4(hi0, hi1, hi2, __int_as_float(from));
 }
 
 }  // namespace
@@ -702,6 +727,11 @@ namespace rtk {
 
 hipError_t launch_build_cut(const BvhNode4 *nodes, CutTable *out, hipStream_t stream) {
     hipLaunchKernelGGL(build_cut_kernel, dim3(1), dim3(64), 0, stream, nodes, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_refresh_cut(const BvhNode4 *nodes, CutTable *out, hipStream_t stream) {
+    hipLaunchKernelGGL(refresh_cut_kernel, dim3(1), dim3(64), 0, stream, nodes, out);
     return hipGetLastError();
 }
 
