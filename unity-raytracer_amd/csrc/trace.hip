@@ -254,7 +254,11 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     return col;
 }
 
+#ifdef RT_EXP_MKWAVES
+constexpr int kMkMinWaves = RT_EXP_MKWAVES;  // measuring builds only
+#else
 constexpr int kMkMinWaves = 5;  // waves per SIMD the register budget must allow (96 VGPRs)
+#endif
 // Waves per megakernel workgroup.  A workgroup's slot is recycled only when
 // all of its waves are done, and path lengths vary a lot between tiles, so
 // small workgroups keep the CUs fuller near the end of each wave "round".
