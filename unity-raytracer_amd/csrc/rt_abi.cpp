@@ -758,8 +758,16 @@ constexpr int kSplitDiv = 256;  // 1/kSplitDiv of the tiles (the slowest) run as
 // their slowest 1/4096 into sixteenth-waves: single frame -15..-30 %,
 // throughput with frames in flight +2..4 % on a 1/4 shard; a whole frame
 // (129,600 tiles) loses 2-6 % and does not split.
+#ifdef RT_EXP_SPLITMAX
+constexpr int kSplitMaxTiles = RT_EXP_SPLITMAX;  // measuring builds only
+#else
 constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this many tiles
+#endif
+#ifdef RT_EXP_SPLIT16MAX
+constexpr int kSplit16MaxTiles = RT_EXP_SPLIT16MAX;  // measuring builds only
+#else
 constexpr int kSplit16MaxTiles = 70000;
+#endif
 constexpr int kSplit16DivLarge = 4096;
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
