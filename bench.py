@@ -65,6 +65,26 @@ def logical_bytes(st, res_x, local_rows):
             + 16 * st.shading_fetches + 16 * res_x * local_rows)
 
 
+def canonical_check(config, st, whole_frame):
+    """The counting launch's counts against the canonical per-config counts
+    committed in profiles/canonical_counts.json (tools/canonical_counts.py: the
+    CPU oracle's walk of the same tree).  Whole frames only."""
+    p = os.path.join(ROOT, "profiles", "canonical_counts.json")
+    if not whole_frame:
+        return {"state": "n/a (row band)"}
+    if not os.path.exists(p):
+        return {"state": "missing"}
+    e = json.load(open(p)).get(config)
+    if not e:
+        return {"state": "missing"}
+    keys = ("primary_rays", "shadow_rays", "reflection_rays", "box_tests", "triangle_tests", "sphere_tests",
+            "shading_fetches")
+    got = {k: int(getattr(st, k)) for k in keys}
+    ok = all(got[k] == e["counts"][k] for k in keys)
+    return {"state": "match" if ok else "mismatch", "committed_logical_bytes": e["logical_bytes_per_frame"],
+            **({} if ok else {"got": got, "committed": e["counts"]})}
+
+
 def lib_sha256(path):
     h = hashlib.sha256()
     with open(path, "rb") as f:
@@ -517,6 +537,7 @@ def main():
                               flags=rt.abi.RT_FLAG_COUNT_TESTS | mode_flags)
     cst = ctx.render_device(fr.camera, fr.plane, cparams, out.data_ptr(), nbytes)
     logical = logical_bytes(cst, rx, local_rows)
+    canonical = canonical_check(fr.name, cst, band_count == 1)
     scene_misses = int(cst.primary_scene_misses)
 
     # setup, untimed: one frame on each stream before the W warmup steps.  A
@@ -696,7 +717,7 @@ def main():
                 # rank 0's host time per enqueued frame: near ms_per_step means host-bound
                 "host_enqueue_ms_per_frame": host_s / args.steps * 1e3,
             },
-            "roofline": roofline(pmc, pmc_state, kname, avg_kernel_s, logical),
+            "roofline": {**roofline(pmc, pmc_state, kname, avg_kernel_s, logical), "canonical_counts": canonical},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(rt, fr, args.cpu_seconds, ctx)

@@ -139,7 +139,7 @@ namespace RayTracer.Native
         public const int OK = 0;
         public const int BuildSahHost = 0, BuildLbvhGpu = 1, BuildLbvhGpuBvh2 = 2, BuildSahRefit = 3;
         public const int FlagCountTests = 1, FlagWavefront = 2, FlagPacket = 4, FlagOutRgba8 = 8, FlagOutRgba16F = 16,
-                         FlagAsync = 32, FlagRowOrder = 64;
+                         FlagAsync = 32, FlagRowOrder = 64, FlagNoCut = 256;
 
         [DllImport(Lib)] public static extern int rt_abi_version();
         public const int GatherNone = 0, GatherPeerCopy = 1, GatherRccl = 2;
@@ -192,6 +192,7 @@ namespace RayTracer.Native
         [DllImport(Lib)] public static extern int rt_intersect_rays(IntPtr ctx, [In] RtRay[] rays, int n,
                                                                    [Out] RtHit[] hits);
         [DllImport(Lib)] public static extern float rt_spec_threshold();
+        [DllImport(Lib)] public static extern int rt_debug_set(IntPtr ctx, int what, int value);  // tests only
 
         public static string LastError(IntPtr ctx) => Marshal.PtrToStringAnsi(rt_last_error(ctx));
 

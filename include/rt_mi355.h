@@ -165,6 +165,10 @@ typedef struct rt_render_params {
  * few frames).  This flag keeps row-major order.  Results never depend on the
  * order. */
 #define RT_FLAG_ROW_ORDER   64
+/* Camera packets start at the root instead of below the tree's top-level cut
+ * (DESIGN.md §5): the reference ordering of node visits, for testing that the
+ * cut changes no result.  Results never depend on it. */
+#define RT_FLAG_NO_CUT      256
 
 /* Work counters and timings of the last render. */
 typedef struct rt_stats {
@@ -407,6 +411,13 @@ int rt_intersect_rays(rt_ctx *ctx, const rt_ray *rays, int32_t n, rt_hit *out_hi
  * (RayTracingSetup.cs:384-392), which the kernels use instead of acos so the
  * discrete specular branch matches the host libm bit for bit. */
 float rt_spec_threshold(void);
+
+/* Testing only (fault injection; no reference counterpart): what = 
+ * RT_DEBUG_FAIL_SLAB makes rt_render's host-output pipeline fail before row
+ * slab `value` (-1: off), so the error path's cleanup — every copy posted
+ * for the earlier slabs finished before rt_render returns — can be tested. */
+#define RT_DEBUG_FAIL_SLAB 1
+int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value);
 
 #ifdef __cplusplus
 }

@@ -425,6 +425,18 @@ static rt_hit bvh_intersect(const orc_bvh *B, const rt_scene_desc *sc, const rt_
  * reference rank), the exact Mesh.AABB gate per leaf (Scene.cs:67), and
  * shadow rays as any-hit queries with the predicate t*t < d2.  Same answers as
  * the brute-force scan (the GPU parity tests hold that for this tree).
+ *
+ * The walk restates the GPU's per-lane traversal step for step
+ * (unity-raytracer_amd/csrc/traverse.h trav_step, as the counting launch
+ * RT_FLAG_COUNT_TESTS runs it): the exact node test (plane - o) * (1/d) per
+ * child (child_key_exact), the children ordered by the same five-comparator
+ * network on their entry distances (misses = +inf; closest-hit and any-hit
+ * queries alike), the hit ones pushed far-first, triangle leaves tested in
+ * order with an early exit on an occluder, and the mesh gate re-evaluated
+ * whenever a leaf of another mesh than the last evaluated one is reached.  So
+ * its box / triangle / sphere / shading counts are the canonical counts
+ * SURVEY §8(d) prices, and the GPU counting launch must reproduce them
+ * exactly (tests/test_gpu_counts.py).
  * --------------------------------------------------------------------- */
 typedef struct { float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4]; int32_t child[4], pad[4]; } orc_node4;
 typedef struct { float p0[4], p1[4], p2[4]; } orc_trirec;  /* v0 e1.x | e1.yz e2.xy | e2.z rank gate - */
@@ -473,12 +485,7 @@ static int bvh4_query(const orc_bvh4 *B, const rt_scene_desc *sc, const rt_aabb 
     *rank_out = -1;
     ct->box++;
     if (B->nnodes == 0 || !orc_ray_aabb(ray, scene_box)) return 0; /* Scene.cs:54 */
-    if (t_gate_n < B->mesh_count) {
-        free(t_gate);
-        t_gate = (unsigned long long *)calloc((size_t)B->mesh_count, sizeof *t_gate);
-        t_gate_n = B->mesh_count;
-    }
-    const unsigned long long stamp = ++t_stamp;
+    int gate_cached = -1, gate_ok = 0; /* the last mesh whose gate was evaluated (traverse.h Trav) */
     const float o[3] = {ray->origin.x, ray->origin.y, ray->origin.z};
     const float inv[3] = {1.0f / ray->direction.x, 1.0f / ray->direction.y, 1.0f / ray->direction.z};
     float best = FLT_MAX, cull = any ? tlimit : FLT_MAX;
@@ -489,24 +496,30 @@ static int bvh4_query(const orc_bvh4 *B, const rt_scene_desc *sc, const rt_aabb 
             const orc_node4 *nd = &B->nodes[ref];
             const float *lo[3] = {nd->lox, nd->loy, nd->loz}, *hi[3] = {nd->hix, nd->hiy, nd->hiz};
             float key[4];
-            int ch[4], nh = 0;
-            for (int c = 0; c < 4; ++c) {
-                float tn = 0.0f, tf = cull;
-                for (int a = 0; a < 3; ++a) { /* padded box; NaN operands ignored */
-                    const float t1 = (lo[a][c] - o[a]) * inv[a], t2 = (hi[a][c] - o[a]) * inv[a];
-                    tn = fmaxf(tn, fminf(t1, t2));
-                    tf = fminf(tf, fmaxf(t1, t2));
+            int ch[4];
+            for (int c = 0; c < 4; ++c) { /* child_key_exact: padded box; NaN operands ignored */
+                float t1[3], t2[3];
+                for (int a = 0; a < 3; ++a) {
+                    t1[a] = (lo[a][c] - o[a]) * inv[a];
+                    t2[a] = (hi[a][c] - o[a]) * inv[a];
                 }
+                const float tn = fmaxf(fmaxf(fminf(t1[0], t2[0]), fminf(t1[1], t2[1])), fmaxf(fminf(t1[2], t2[2]), 0.0f));
+                const float tf = fminf(fminf(fmaxf(t1[0], t2[0]), fmaxf(t1[1], t2[1])), fminf(fmaxf(t1[2], t2[2]), cull));
                 ct->box++;
-                if (tn <= tf) {
-                    /* insertion by entry distance: near first (any-hit: slot order) */
-                    int k = nh++;
-                    while (!any && k > 0 && key[k - 1] > tn) { key[k] = key[k - 1]; ch[k] = ch[k - 1]; --k; }
-                    key[k] = tn;
-                    ch[k] = nd->child[c];
+                key[c] = tn <= tf ? tn : INFINITY;
+                ch[c] = nd->child[c];
+            }
+            /* the GPU's sorting network (traverse.h RT_CSWAP order), swap iff k[j] < k[i] */
+            static const int net[5][2] = {{0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}};
+            for (int s = 0; s < 5; ++s) {
+                const int i = net[s][0], j = net[s][1];
+                if (key[j] < key[i]) {
+                    const float tk = key[i]; key[i] = key[j]; key[j] = tk;
+                    const int tc = ch[i]; ch[i] = ch[j]; ch[j] = tc;
                 }
             }
-            if (nh == 0) goto pop;
+            if (key[0] == INFINITY) goto pop;
+            const int nh = 1 + (key[1] != INFINITY) + (key[2] != INFINITY) + (key[3] != INFINITY);
             for (int k = nh - 1; k >= 1; --k) stack[sp++] = ch[k];
             ref = ch[0];
             continue;
@@ -520,13 +533,12 @@ static int bvh4_query(const orc_bvh4 *B, const rt_scene_desc *sc, const rt_aabb 
                     const int gate = rbits(r->p2[2]);
                     rank = rbits(r->p2[1]);
                     if (gate >= 0) {
-                        unsigned long long g = t_gate[gate];
-                        if ((g >> 1) != stamp) { /* Mesh.AABB gate, Scene.cs:67, once per ray and mesh */
+                        if (gate != gate_cached) { /* Mesh.AABB gate, Scene.cs:67 */
                             ct->box++;
-                            g = (stamp << 1) | (unsigned long long)(orc_ray_aabb(ray, &sc->meshes[gate].aabb) != 0);
-                            t_gate[gate] = g;
+                            gate_cached = gate;
+                            gate_ok = orc_ray_aabb(ray, &sc->meshes[gate].aabb) != 0;
                         }
-                        if (!(g & 1)) continue;
+                        if (!gate_ok) continue;
                     }
                     ct->tri++;
                     /* RMath.RayTriangleIntersection :29-73 on the stored edges (v1 - v0, v2 - v0) */

@@ -2,12 +2,11 @@
 build_cut_kernel): a tile's camera packet starts from the cut entries its
 widened frustum touches, and waiting entries are re-tested against each lane's
 closest hit when popped.  Only the visiting order may change, so frames must
-be bit-identical with the cut switched off (RT_NO_CUT, every packet from the
+be bit-identical with the cut switched off (RT_FLAG_NO_CUT, every packet from the
 root) and equal to the oracle — including scenes far from the origin (the
 frustum test's slack), cameras inside the geometry, partial edge tiles, split
 waves (longest-first quarter/sixteenth waves of small shards), row bands and
 row slabs, and the device-built trees."""
-import os
 
 import numpy as np
 import pytest
@@ -20,14 +19,9 @@ TOL = 1e-4
 
 
 def _render(ctx, rt, fr, build=0, cut=True, **kw):
-    os.environ.pop("RT_NO_CUT", None)
     if not cut:
-        os.environ["RT_NO_CUT"] = "1"
-    try:
-        img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
-    finally:
-        os.environ.pop("RT_NO_CUT", None)
-    return img, st
+        kw["flags"] = kw.get("flags", 0) | rt.abi.RT_FLAG_NO_CUT
+    return ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
 
 
 def _same(a, b):

@@ -31,6 +31,8 @@ RT_FLAG_OUT_RGBA16F = 16
 RT_FLAG_OUT_RGB32F = 128
 RT_FLAG_ASYNC = 32
 RT_FLAG_ROW_ORDER = 64
+RT_FLAG_NO_CUT = 256
+RT_DEBUG_FAIL_SLAB = 1
 RT_BUILD_SAH_HOST = 0
 RT_BUILD_LBVH_GPU = 1
 RT_BUILD_LBVH_GPU_BVH2 = 2
@@ -225,6 +227,7 @@ SIGNATURES = {
     "rt_synchronize": (C.c_int, [_P]),
     "rt_assemble_bands_ex": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_intersect_rays": (C.c_int, [_P, _P, C.c_int32, _P]),
+    "rt_debug_set": (C.c_int, [_P, C.c_int32, C.c_int32]),
 }
 
 _lib = None

@@ -152,11 +152,35 @@ struct CutStart {
 // cut_*): every camera ray of the tile (RayTracingSetup.cs:291-296, rounded)
 // lies at least a pixel inside them.  Writes the entries below the top two
 // into wstack.  Every lane of the wave must be active (one entry per lane).
+// One lane's cut entry (lane j holds entry j), loaded before the tile is
+// known: the loads overlap the tile's own setup instead of following it.
+struct CutLane {
+    int n_all;
+    f3 lo, hi;
+    int ref;
+};
+
+__device__ __forceinline__ CutLane cut_load(const rtd::SceneDev &S) {
+    CutLane c;
+    const rtd::CutTable *T = S.cut;
+    c.n_all = T ? rtt::cload(&T->count) : 0;
+    const int j = rtt::lane_id() & (rtd::kCutMax - 1);
+    if (T) {
+        c.lo = mk(T->lo_x[j], T->lo_y[j], T->lo_z[j]);
+        c.hi = mk(T->hi_x[j], T->hi_y[j], T->hi_z[j]);
+        c.ref = T->ref[j];
+    } else {
+        c.lo = c.hi = mk(0.0f, 0.0f, 0.0f);
+        c.ref = 0;
+    }
+    return c;
+}
+
 __device__ __forceinline__ CutStart cut_select(const rtd::SceneDev &S, const rtd::FrameDev &F, const TileRect &tr,
-                                               int *wstack) {
+                                               int *wstack, const CutLane *pre = nullptr) {
     CutStart cs = {0, 0, 0, -1};
     const rtd::CutTable *T = S.cut;
-    const int n_all = rtt::cload(&T->count);
+    const int n_all = pre ? pre->n_all : rtt::cload(&T->count);
     if (n_all <= 0) return cs;
     const int j = rtt::lane_id();
     bool need = false;
@@ -166,8 +190,9 @@ __device__ __forceinline__ CutStart cut_select(const rtd::SceneDev &S, const rtd
         const float xa = (float)(tr.x0 - 1), xb = (float)(tr.x0 + tr.w + 1);
         const float ya = (float)(tr.y0 - 1), yb = (float)(tr.y0 + tr.h + 1);
         const f3 o = rtt::ld3(F.cam_pos);
-        const f3 lo = mk(T->lo_x[j], T->lo_y[j], T->lo_z[j]), hi = mk(T->hi_x[j], T->hi_y[j], T->hi_z[j]);
-        ref = T->ref[j];
+        const f3 lo = pre ? pre->lo : mk(T->lo_x[j], T->lo_y[j], T->lo_z[j]);
+        const f3 hi = pre ? pre->hi : mk(T->hi_x[j], T->hi_y[j], T->hi_z[j]);
+        ref = pre ? pre->ref : T->ref[j];
         const f3 clo = lo - o, chi = hi - o;
         const f3 ax = rtt::ld3(F.cut_ax), bx = rtt::ld3(F.cut_bx), ay = rtt::ld3(F.cut_ay), by = rtt::ld3(F.cut_by);
         const f3 nx0 = mk(fmaf(xa, bx.x, ax.x), fmaf(xa, bx.y, ax.y), fmaf(xa, bx.z, ax.z));
@@ -219,10 +244,15 @@ __device__ __forceinline__ CutStart cut_select(const rtd::SceneDev &S, const rtd
 // ANY: shadow query with predicate t*t < d2 (see traverse.h).  `part`: the
 // lane takes part.  wstack: this wave's LDS stack (kWaveStack ints).
 // cs (camera packets): the start cut_select chose (null or state -1: the root).
+// hint (ANY, < 0: a leaf ref): a leaf to test first — the one that occluded
+// the most lanes of this tile's shadow packet last time; the walk from the
+// root then never visits it again (each live lane has tested it already, and
+// any-hit order cannot change an answer).  hint_out: where the leaf that
+// retires the most lanes this time is stored (0: none), by one lane.
 template <bool ANY, bool COUNT>
 __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCtx &r, bool part, float tlimit,
                                              float d2, PacketLane &L, int *wstack, Counts &cnt,
-                                             const CutStart *cs = nullptr) {
+                                             const CutStart *cs = nullptr, int hint = 0, int *hint_out = nullptr) {
     L.best_t = FLT_MAX;
     L.best_rank = -1;
     L.tcull = ANY ? tlimit : FLT_MAX;
@@ -262,6 +292,55 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
     const bool same_signs = (mx == 0 || mx == live0) && (my == 0 || my == live0) && (mz == 0 || mz == live0);
     // plane-row offsets in the node (lo, hi per axis): near row first
     const int ox = uni(same_signs && mx != 0), oy = uni(same_signs && my != 0), oz = uni(same_signs && mz != 0);
+    // one leaf (ref < 0) against every live lane
+    auto visit_leaf = [&](int ref) {
+        const int v = ~ref;
+        const int first = v & ((1 << rtd::kLeafFirstBits) - 1);
+        const int count = ((v >> rtd::kLeafFirstBits) & 3) + 1;
+        const int kind = (v >> (rtd::kLeafFirstBits + 2)) & 1;
+        if (kind == rtd::kLeafTri) {
+            packet_leaf_tris<ANY, COUNT>(S, r, L, wgate, d2, first, count, cnt);
+        } else {
+            const int gate = rtt::cload(&S.sphs[first].misc).y;
+            if (L.live) {
+                rtt::Trav t;
+                t.best_t = L.best_t;
+                t.best_rank = L.best_rank;
+                t.tcull = L.tcull;
+                t.gate_cached = L.gate_cached;
+                t.gate_ok = L.gate_ok;
+                const bool occ = rtt::leaf<ANY, COUNT, true>(S, r, t, d2, first, count, kind, gate, cnt);
+                L.best_t = t.best_t;
+                L.best_rank = t.best_rank;
+                L.tcull = t.tcull;
+                L.gate_cached = t.gate_cached;
+                L.gate_ok = t.gate_ok;
+                if (ANY && occ) L.live = false;
+            }
+            if (gate >= 0) wgate = -2;  // the lanes' caches moved on their own
+        }
+    };
+#ifdef RT_EXP_LASTOCC
+    // any-hit: the leaf that retires the most lanes (the next frame's hint)
+    int best_leaf = 0, best_retired = 0;  // wave-uniform
+    int skip = 0;                         // the hinted leaf, never visited again
+    auto note_hint = [&]() {
+        if (!ANY || !hint_out) return;
+        if (rtt::lane_id() == __ffsll((long long)__ballot(1)) - 1) *hint_out = best_leaf;
+    };
+    if (ANY && hint < 0) {
+        const unsigned long long before = __ballot(L.live);
+        visit_leaf(hint);
+        const unsigned long long after = __ballot(L.live);
+        best_retired = __popcll(before & ~after);
+        best_leaf = best_retired ? hint : 0;
+        if (after == 0) {
+            note_hint();
+            return;
+        }
+        skip = hint;
+    }
+#endif
     while (true) {
         if (!ANY && node >= kCutMark) {
             // a waiting cut entry (cut_select): visited only if a live lane's
@@ -316,8 +395,15 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                 // any-hit (shadow rays): the order cannot change the answer,
                 // so the children any live lane needs are taken in slot order
                 // without the wave-wide sort (C3 -6 %, C2 -3 %, C5 +-0)
+#ifdef RT_EXP_LASTOCC
+                const bool n0 = __ballot(k0 != INFINITY) != 0 && ch.x != skip,
+                           n1 = __ballot(k1 != INFINITY) != 0 && ch.y != skip,
+                           n2 = __ballot(k2 != INFINITY) != 0 && ch.z != skip,
+                           n3 = __ballot(k3 != INFINITY) != 0 && ch.w != skip;
+#else
                 const bool n0 = __ballot(k0 != INFINITY) != 0, n1 = __ballot(k1 != INFINITY) != 0,
                            n2 = __ballot(k2 != INFINITY) != 0, n3 = __ballot(k3 != INFINITY) != 0;
+#endif
                 int nn = 0, nxt = 0;
                 if (n3) { nxt = ch.w; ++nn; }
                 if (n2) { if (nn) RT_PK_PUSH(nxt); nxt = ch.z; ++nn; }
@@ -364,34 +450,32 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             }
             }
         } else {
-            const int v = ~node;
-            const int first = v & ((1 << rtd::kLeafFirstBits) - 1);
-            const int count = ((v >> rtd::kLeafFirstBits) & 3) + 1;
-            const int kind = (v >> (rtd::kLeafFirstBits + 2)) & 1;
-            if (kind == rtd::kLeafTri) {
-                packet_leaf_tris<ANY, COUNT>(S, r, L, wgate, d2, first, count, cnt);
-            } else {
-                const int gate = rtt::cload(&S.sphs[first].misc).y;
-                if (L.live) {
-                    rtt::Trav t;
-                    t.best_t = L.best_t;
-                    t.best_rank = L.best_rank;
-                    t.tcull = L.tcull;
-                    t.gate_cached = L.gate_cached;
-                    t.gate_ok = L.gate_ok;
-                    const bool occ = rtt::leaf<ANY, COUNT, true>(S, r, t, d2, first, count, kind, gate, cnt);
-                    L.best_t = t.best_t;
-                    L.best_rank = t.best_rank;
-                    L.tcull = t.tcull;
-                    L.gate_cached = t.gate_cached;
-                    L.gate_ok = t.gate_ok;
-                    if (ANY && occ) L.live = false;
+#ifdef RT_EXP_LASTOCC
+            const unsigned long long before = ANY ? __ballot(L.live) : 0ull;
+            visit_leaf(node);
+            if (ANY) {
+                const unsigned long long after = __ballot(L.live);
+                const int retired = __popcll(before & ~after);
+                if (retired > best_retired) {
+                    best_retired = retired;
+                    best_leaf = node;
                 }
-                if (gate >= 0) wgate = -2;  // the lanes' caches moved on their own
+                if (after == 0) {
+                    note_hint();
+                    return;
+                }
             }
+#else
+            visit_leaf(node);
             if (ANY && __ballot(L.live) == 0) return;
+#endif
         }
-        if (sp == 0) return;
+        if (sp == 0) {
+#ifdef RT_EXP_LASTOCC
+            note_hint();
+#endif
+            return;
+        }
         --sp;
         node = uni(topv);
         if (sp > 0) topv = wstack[sp - 1];

@@ -39,6 +39,8 @@ constexpr int kWavesPerBlock = kBlockThreads / kWaveSize;
 constexpr int kCounterSlots = 256;
 constexpr int kCounterWords = 16;  // one 128-B slot: words 0-8 used (rt_stats order)
 
+constexpr int kHintLights = 4;  // lights whose first shadow packets keep an occluder hint (FrameDev::shadow_hint)
+
 constexpr int kLeafTri = 0;
 constexpr int kLeafSphere = 1;
 
@@ -212,6 +214,9 @@ struct FrameDev {
     int row0;                // band_count == 1: first image row of this launch (a row slab of rt_render)
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
+    unsigned tiles_x_magic;  // floor(2^32 / tiles_x) (0xffffffff for 1): tile -> (tx, ty) without a division
+    int *shadow_hint;        // render_kernel: per tile x light (< kHintLights) the leaf that occluded the most
+                             // lanes of the tile's first shadow packet last time (0: none); null: off
     void *out;               // local_rows x res_x pixels in out_format
     const int *tile_order;   // megakernel dispatch order (null: row-major)
     unsigned *tile_cost;     // per-tile cost of this frame (shader clock), null: not recorded

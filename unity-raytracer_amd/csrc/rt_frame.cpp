@@ -1,0 +1,657 @@
+// rt_frame.cpp — one frame: CastPixelRays' constants (RayTracingSetup.cs:
+// 275-302, ImagePlane.cs:26-44), the conservative sky test and tile frustum
+// constants, longest-first tile dispatch, the trace launches, the sharded ray
+// counters, RT_FLAG_ASYNC bookkeeping and rt_render's host-output pipeline
+// (row slabs on two streams, copies from a thread of their own).
+#include "rt_host.h"
+
+namespace rti {
+
+int isqrt_exact(int v) {
+    if (v <= 0) return -1;
+    int n = 1;
+    while (n * n < v) ++n;
+    return n * n == v ? n : -1;
+}
+
+// The conservative sky test's per-frame constants (rt_device.h FrameDev
+// sky_*), in double: the Scene.AABB padded by 2^-10 of the camera-relative
+// scene scale.  An exact sample ray that passes the exact gate (RMath.cs:12-26)
+// comes geometrically within ~1e-7 of that scale of the box; the kernel's
+// approximate ray deviates by ~1e-6 of it; the pad is ~1e-3 of it.  Off when
+// anything is non-finite or the camera is inside the padded box (every ray
+// may then enter it).
+void sky_setup(const rtd::SceneDev &S, rtd::FrameDev &F) {
+    F.sky_test = 0;
+    if (!S.has_prims || F.res_x <= 0 || F.res_y <= 0) return;
+    double lo[3], hi[3], c[3], scale = 0.0;
+    bool finite = std::isfinite(F.hl) && std::isfinite(F.vl);
+    for (int a = 0; a < 3; ++a) {
+        c[a] = F.cam_pos[a];
+        lo[a] = (double)S.scene_lo[a] - c[a];
+        hi[a] = (double)S.scene_hi[a] - c[a];
+        finite = finite && std::isfinite(lo[a]) && std::isfinite(hi[a]) && lo[a] <= hi[a] &&
+                 std::isfinite(F.top_left[a]) && std::isfinite(F.right[a]) && std::isfinite(F.up[a]);
+        scale = std::max(scale, std::max(std::fabs(lo[a]), std::fabs(hi[a])));
+    }
+    if (!finite) return;
+    const double pad = std::ldexp(std::max(scale, 1e-30), -10);
+    bool inside = true;
+    for (int a = 0; a < 3; ++a) {
+        lo[a] -= pad;
+        hi[a] += pad;
+        inside = inside && lo[a] <= 0.0 && hi[a] >= 0.0;
+        F.sky_lo[a] = (float)lo[a];
+        F.sky_hi[a] = (float)hi[a];
+        F.sky_tlc[a] = (float)((double)F.top_left[a] - c[a]);
+    }
+    if (inside) return;
+    // rounding the padded bounds to float moves them by far less than the pad
+    F.sky_hx = (float)((double)F.hl / F.res_x);
+    F.sky_vy = (float)((double)F.vl / F.res_y);
+    F.sky_test = 1;
+}
+
+// The camera packets' tile frustum (FrameDev cut_*, packet.h cut_start):
+// D(x, y) = A + x R + y U; the plane through the camera spanned by D(xa, .)
+// has the normal cross(A + xa R, U) = cross(A, U) + xa cross(R, U), on the
+// side x >= xa when multiplied by sign(det[A, U, R]); likewise y with
+// cross(A + ya U, R) and sign(det[A, R, U]).  Computed in double, rounded.
+void cut_setup(const rtd::SceneDev &S, rtd::FrameDev &F, bool no_cut) {
+    F.cut_test = 0;
+    if (!S.cut || !S.bvh4 || !S.has_prims || F.res_x <= 0 || F.res_y <= 0) return;
+    if (no_cut) return;  // RT_FLAG_NO_CUT: every camera packet from the root
+    // a tile's rows must lie in one band block (contiguous image rows)
+    if (F.band_count > 1 && F.band_rows % F.tile_h != 0) return;
+    double A[3], R[3], U[3];
+    for (int a = 0; a < 3; ++a) {
+        A[a] = (double)F.top_left[a] - (double)F.cam_pos[a];
+        R[a] = (double)F.right[a] * F.hl / F.res_x;
+        U[a] = -(double)F.up[a] * F.vl / F.res_y;
+    }
+    auto cross = [](const double *p, const double *q, double *o) {
+        o[0] = p[1] * q[2] - p[2] * q[1];
+        o[1] = p[2] * q[0] - p[0] * q[2];
+        o[2] = p[0] * q[1] - p[1] * q[0];
+    };
+    double aU[3], rU[3], aR[3], uR[3];
+    cross(A, U, aU);
+    cross(R, U, rU);
+    cross(A, R, aR);
+    cross(U, R, uR);
+    const double det = aU[0] * R[0] + aU[1] * R[1] + aU[2] * R[2];  // det[A, U, R]
+    bool finite = std::isfinite(det) && det != 0.0;
+    const double sx = det > 0.0 ? 1.0 : -1.0, sy = -sx;  // det[A, R, U] = -det[A, U, R]
+    for (int a = 0; a < 3; ++a) {
+        F.cut_ax[a] = (float)(sx * aU[a]);
+        F.cut_bx[a] = (float)(sx * rU[a]);
+        F.cut_ay[a] = (float)(sy * aR[a]);
+        F.cut_by[a] = (float)(sy * uR[a]);
+        F.cut_a[a] = (float)A[a];
+        F.cut_r[a] = (float)R[a];
+        F.cut_u[a] = (float)U[a];
+        finite = finite && std::isfinite(F.cut_ax[a]) && std::isfinite(F.cut_bx[a]) && std::isfinite(F.cut_ay[a]) &&
+                 std::isfinite(F.cut_by[a]) && std::isfinite(F.cam_pos[a]);
+    }
+    F.cut_test = finite ? 1 : 0;
+}
+
+int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, const rt_render_params *prm,
+                  rtd::FrameDev &F, size_t &out_bytes) {
+    if (!cam || !plane || !prm) return fail(ctx, RT_E_INVALID, "null camera/plane/params");
+    if (!ctx->has_scene) return fail(ctx, RT_E_STATE, "rt_render before rt_set_scene");
+    if (plane->resolution_x < 0 || plane->resolution_y < 0)
+        return fail(ctx, RT_E_INVALID, "negative resolution (%d, %d)", plane->resolution_x, plane->resolution_y);
+    const int n = isqrt_exact(prm->samples_per_pixel);
+    if (n < 0 || n > 8)
+        return fail(ctx, RT_E_INVALID, "samples_per_pixel must be n*n with 1 <= n <= 8, got %d",
+                    prm->samples_per_pixel);
+    const int band_count = prm->band_count <= 0 ? 1 : prm->band_count;
+    const int band_rows = prm->band_rows <= 0 ? 8 : prm->band_rows;
+    if (prm->band_index < 0 || prm->band_index >= band_count)
+        return fail(ctx, RT_E_INVALID, "band_index %d outside [0, %d)", prm->band_index, band_count);
+    std::memset(&F, 0, sizeof F);
+    // ImagePlane.GetRect(cameraData).TopLeft (ImagePlane.cs:26-44)
+    const rtm::f3 center = F3(cam->position) + F3(cam->forward) * plane->distance_to_camera;
+    const rtm::f3 half_up = F3(cam->up) * plane->half_vertical_length;
+    const rtm::f3 half_right = F3(cam->right) * plane->half_horizontal_length;
+    const rtm::f3 tl = (center - half_right) + half_up;
+    F.cam_pos[0] = cam->position.x; F.cam_pos[1] = cam->position.y; F.cam_pos[2] = cam->position.z;
+    F.right[0] = cam->right.x; F.right[1] = cam->right.y; F.right[2] = cam->right.z;
+    F.up[0] = cam->up.x; F.up[1] = cam->up.y; F.up[2] = cam->up.z;
+    F.top_left[0] = tl.x; F.top_left[1] = tl.y; F.top_left[2] = tl.z;
+    F.hl = plane->half_horizontal_length * 2.0f;  // HorizontalLength, ImagePlane.cs:23
+    F.vl = plane->half_vertical_length * 2.0f;
+    for (int i = 0; i < 3; ++i) F.bg255[i] = prm->background_color[i] * 255.0f;  // Rgb(Color), Rgb.cs:15-18
+    F.res_x = plane->resolution_x;
+    F.res_y = plane->resolution_y;
+    F.spp = n * n;
+    F.spp_n = n;
+    F.inv_spp = 1.0f / (float)F.spp;
+    F.max_bounces = prm->max_reflection_bounces;
+    F.band_index = prm->band_index;
+    F.band_count = band_count;
+    F.band_rows = band_rows;
+    F.local_rows = band_local_rows(F.res_y, band_count, band_rows);
+    // tile: 64/spp pixels per wave; a power of two is laid out as a
+    // near-square 2^a x 2^b block
+    const int ppw = rtd::kWaveSize / F.spp;
+    int tw = ppw, th = 1;
+    if ((ppw & (ppw - 1)) == 0) {
+        int lg = 0;
+        while ((1 << lg) < ppw) ++lg;
+        th = 1 << (lg / 2);
+        tw = ppw / th;
+    }
+    F.tile_w = tw;
+    F.tile_h = th;
+    F.tiles_x = (F.res_x + tw - 1) / tw;
+    F.tiles_x_magic = F.tiles_x <= 1 ? 0xffffffffu : (unsigned)((1ull << 32) / (unsigned long long)F.tiles_x);
+    const int tiles_y = (F.local_rows + th - 1) / th;
+    F.num_tiles = F.res_x > 0 ? F.tiles_x * tiles_y : 0;
+    const bool f8 = (prm->flags & RT_FLAG_OUT_RGBA8) != 0, f16 = (prm->flags & RT_FLAG_OUT_RGBA16F) != 0,
+               f12 = (prm->flags & RT_FLAG_OUT_RGB32F) != 0;
+    if ((int)f8 + (int)f16 + (int)f12 > 1)
+        return fail(ctx, RT_E_INVALID, "RT_FLAG_OUT_RGBA8, RT_FLAG_OUT_RGBA16F and RT_FLAG_OUT_RGB32F are exclusive");
+    F.out_format = f8 ? rtd::kOutRGBA8 : (f16 ? rtd::kOutRGBA16F : (f12 ? rtd::kOutRGB32F : rtd::kOutFloat4));
+    out_bytes = (size_t)F.local_rows * F.res_x * rt_pixel_bytes(prm->flags);
+    sky_setup(ctx->S, F);
+    cut_setup(ctx->S, F, (prm->flags & RT_FLAG_NO_CUT) != 0);
+    return RT_OK;
+}
+
+// Upper bound on wavefront pool entries (64 B each) per chunk: 160M = 10 GB.
+constexpr size_t kPoolBudget = (size_t)160 << 20;
+constexpr size_t kShadowBudget = (size_t)96 << 20;
+
+void free_wavefront(rt_ctx *c) {
+    void *ps[] = {c->wf_ray_o, c->wf_ray_d, c->wf_col, c->wf_sh_o, c->wf_sh_d, c->wf_hit, c->wf_occ};
+    for (void *p : ps)
+        if (p) (void)hipFree(p);
+    c->wf_ray_o = c->wf_ray_d = c->wf_col = c->wf_sh_o = c->wf_sh_d = nullptr;
+    c->wf_hit = nullptr;
+    c->wf_occ = nullptr;
+    c->pool_cap = c->shadow_cap = 0;
+}
+
+// Chunk size (tiles) so that the worst case (every hit a mirror down to the
+// bounce limit) fits the pool budget, and (re)allocation of the queues.
+int prepare_wavefront(rt_ctx *ctx, const rtd::FrameDev &F, int &chunk_tiles, rtw::Args &A) {
+    const size_t levels = (size_t)(F.max_bounces > 0 ? F.max_bounces : 0) + 1;
+    const size_t lights = (size_t)std::max(1, ctx->S.num_lights);
+    size_t tiles = (size_t)std::max(1, F.num_tiles);
+    tiles = std::min(tiles, std::max<size_t>(1, kPoolBudget / (levels * 64)));
+    tiles = std::min(tiles, std::max<size_t>(1, kShadowBudget / (lights * 64)));
+    chunk_tiles = (int)tiles;
+    const size_t pool = tiles * 64 * levels, shadow = tiles * 64 * lights;
+    if (!ctx->wf_ctr) HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ctr, sizeof(rtw::Counters)));
+    if (pool > ctx->pool_cap || shadow > ctx->shadow_cap) {
+        HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+        free_wavefront(ctx);
+        const size_t p = std::max(pool, ctx->pool_cap), q = std::max(shadow, ctx->shadow_cap);
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ray_o, p * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ray_d, p * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_col, p * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_hit, p * sizeof(int4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_sh_o, q * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_sh_d, q * sizeof(float4)));
+        HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_occ, q));
+        ctx->pool_cap = p;
+        ctx->shadow_cap = q;
+    }
+    A.ctr = ctx->wf_ctr;
+    A.ray_o = ctx->wf_ray_o;
+    A.ray_d = ctx->wf_ray_d;
+    A.hit = ctx->wf_hit;
+    A.col = ctx->wf_col;
+    A.sh_o = ctx->wf_sh_o;
+    A.sh_d = ctx->wf_sh_d;
+    A.occ = ctx->wf_occ;
+    A.tile0 = 0;
+    A.n0 = 0;
+    A.max_level = (int)levels - 1;
+    return RT_OK;
+}
+
+
+// Quarter-wave splitting of a frame's slowest tiles trades extra work (each
+// quarter re-walks the BVH top) for a shorter critical path; it pays only
+// when the frame (shard) is small enough for its slowest wave to set its
+// time: measured with 3 frames in flight, a 1/8 C3 shard (16,200 tiles)
+// +18 %, a 1/4 shard (32,400) -7 %, a whole frame (129,600) -7 %.  The very
+// slowest of them (1/2048 of the tiles) go further, to sixteen waves of one
+// pixel each: a 1/8 shard's single frame -14 % more, throughput with frames
+// in flight +-1 % (1/512 or more: -5..-15 %).
+constexpr int kSplit16Div = 2048;  // of those, 1/kSplit16Div of the tiles as sixteenth-waves; 0: off
+constexpr int kSplitDiv = 256;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
+// Larger shards (up to 70,000 tiles: a 1/2 or 1/4 shard of 1080p) split only
+// their slowest 1/4096 into sixteenth-waves: single frame -15..-30 %,
+// throughput with frames in flight +2..4 % on a 1/4 shard; a whole frame
+// (129,600 tiles) loses 2-6 % and does not split.
+#ifdef RT_EXP_SPLITMAX
+constexpr int kSplitMaxTiles = RT_EXP_SPLITMAX;  // measuring builds only
+#else
+constexpr int kSplitMaxTiles = 24000;    // ... in frames/shards of at most this many tiles
+#endif
+#ifdef RT_EXP_SPLIT16MAX
+constexpr int kSplit16MaxTiles = RT_EXP_SPLIT16MAX;  // measuring builds only
+#else
+constexpr int kSplit16MaxTiles = 70000;
+#endif
+constexpr int kSplit16DivLarge = 4096;
+constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
+// rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
+// kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
+// a 0.29 ms frame — small slabs first so the copy starts early, then slabs the render keeps ahead
+// of), else kSlabsRenderBound (RGBA8 / RGBA16F: small last slab, little copy after the render);
+// measured best of 9 / 10 weight vectors on C3 (tools/exp/e2e_weights.py, profiles/r03_e2e/).
+// Frames under kSlabMinFrame go in one piece.
+constexpr double kSlabsCopyBound[] = {1, 2, 2, 3, 3, 4};
+constexpr double kSlabsRenderBound[] = {1, 2, 2, 1};
+constexpr size_t kSlabMinFrame = (size_t)2 << 20;
+constexpr int kMaxSlabs = 16;  // slab count range (RT_EXP_SLAB_WEIGHTS measuring builds)
+
+// Enqueues the sum of the sharded ray/test counters into ctx->h_counts (read
+// after the stream's synchronisation by read_folded).
+int fold_counters(rt_ctx *ctx, hipStream_t stream) {
+    HIP_OR_FAIL(ctx, rtk::launch_fold_counters(ctx->d_counters, ctx->h_counts, stream));
+    return RT_OK;
+}
+
+void read_folded(const rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
+    const volatile unsigned long long *h = ctx->h_counts;
+    for (int w = 0; w < rtd::kCounterWords; ++w) counts[w] = h[w];
+}
+
+// Sums the sharded ray/test counters (the counters' frames must have ended).
+int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
+    int st = fold_counters(ctx, ctx->stream);
+    if (st) return st;
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    read_folded(ctx, counts);
+    return RT_OK;
+}
+
+void fill_stats(rt_stats *stats, const unsigned long long counts[rtd::kCounterWords], double kernel_ms,
+                double total_ms) {
+    stats->primary_rays = counts[0];
+    stats->shadow_rays = counts[1];
+    stats->reflection_rays = counts[2];
+    stats->box_tests = counts[3];
+    stats->triangle_tests = counts[4];
+    stats->sphere_tests = counts[5];
+    stats->shading_fetches = counts[6];
+    stats->primary_scene_misses = counts[7];
+    stats->shadow_rays_moot = counts[8];
+    stats->kernel_ms = kernel_ms;
+    stats->total_ms = total_ms;
+}
+
+// Folds the counters and device time of pending RT_FLAG_ASYNC frames into the
+// context's accumulator (for rt_finish); waits for the stream.
+int settle_async(rt_ctx *ctx) {
+    if (ctx->async_frames == 0) return RT_OK;
+    // the pending frames may sit on several streams (rt_set_stream between them)
+    HIP_OR_FAIL(ctx, hipDeviceSynchronize());
+    unsigned long long counts[rtd::kCounterWords];
+    int st = read_counters(ctx, counts);
+    if (st) return st;
+    for (int w = 0; w < rtd::kCounterWords; ++w) ctx->async_acc[w] += counts[w];
+    // the frames since ev_a0 may have run on several streams: their device
+    // time ends with the last of the streams' final frames
+    float ms = 0.0f;
+    for (auto &se : ctx->async_end) {
+        if (!se.first) continue;
+        float m = 0.0f;
+        HIP_OR_FAIL(ctx, hipEventElapsedTime(&m, ctx->ev_a0, se.second));
+        ms = std::max(ms, m);
+        se.first = nullptr;  // the event object is kept for reuse
+    }
+    ctx->async_ms += ms;
+    ctx->async_frames = 0;
+    return RT_OK;
+}
+
+// Records the end of an RT_FLAG_ASYNC frame on the context's current stream.
+int record_async_end(rt_ctx *ctx) {
+    hipEvent_t ev = nullptr;
+    for (auto &se : ctx->async_end)
+        if (se.first == ctx->stream) ev = se.second;
+    if (!ev) {
+        for (auto &se : ctx->async_end)
+            if (!se.first && !ev) {
+                se.first = ctx->stream;
+                ev = se.second;
+            }
+    }
+    if (!ev) {
+        HIP_OR_FAIL(ctx, hipEventCreate(&ev));
+        ctx->async_end.emplace_back(ctx->stream, ev);
+    }
+    HIP_OR_FAIL(ctx, hipEventRecord(ev, ctx->stream));
+    return RT_OK;
+}
+
+// Longest-first dispatch of a megakernel launch: picks the state of
+// (stream, slab), points F at the last measured order and decides whether
+// this launch measures costs (the caller sorts them after the launch).
+int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool mega, bool count, int slab,
+                LptSlot *&ls, bool &lpt_sort) {
+    ls = nullptr;
+    lpt_sort = false;
+    F.tile_order = nullptr;
+    F.tile_cost = nullptr;
+    F.wave_counts = nullptr;
+    if (!mega || (prm->flags & RT_FLAG_ROW_ORDER) != 0 || F.num_tiles <= 0) return RT_OK;
+    for (LptSlot &l : ctx->lpt)
+        if (l.used && l.stream == ctx->stream && l.slab == slab) ls = &l;
+    if (!ls)
+        for (LptSlot &l : ctx->lpt)
+            if (!l.used && !ls) {
+                ls = &l;
+                ls->used = true;
+                ls->stream = ctx->stream;
+                ls->slab = slab;
+            }
+    if (!ls) return RT_OK;  // more (stream, slab) pairs than slots: row-major order
+    const long long key = ((long long)F.num_tiles << 32) ^ ((long long)F.tiles_x << 20) ^ ((long long)F.spp << 12) ^
+                          ((long long)F.band_count << 6) ^ F.band_index ^ ((long long)F.row0 << 44);
+    if (key != ls->key) {
+        const size_t n = (size_t)F.num_tiles;
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->cost, n * 4));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->cost_sorted, n * 4));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->order, n * 4));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->scratch, rtk::tile_sort_scratch_bytes(F.num_tiles)));
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->iota, n * 4));
+        HIP_OR_FAIL(ctx, rtk::launch_iota((int *)ls->iota.p, F.num_tiles, ctx->stream));
+        ls->key = key;
+        ls->valid = false;
+    }
+    bool hints_stale = false;
+    if (ls->scene != ctx->scene_version) {
+        // a new or updated scene (rt_update_mesh_transforms every Update): the
+        // last order stays a valid permutation of the tiles and, animation being
+        // temporally coherent, a good one — keep dispatching by it and keep the
+        // re-sort period (re-sorting after every update cost ~55 us a frame)
+        ls->scene = ctx->scene_version;
+        hints_stale = true;  // leaf refs of another tree may lie outside this one's arrays
+    }
+#ifdef RT_EXP_LASTOCC
+    {
+        const size_t hb = (size_t)F.num_tiles * rtd::kHintLights * sizeof(int);
+        if (hb > ls->hints.cap) {
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->hints, hb));
+            hints_stale = true;
+        }
+        if (hints_stale) HIP_OR_FAIL(ctx, hipMemsetAsync(ls->hints.p, 0, hb, ctx->stream));
+        F.shadow_hint = count ? nullptr : (int *)ls->hints.p;
+    }
+#else
+    (void)hints_stale;
+#endif
+    if (!ls->valid) ls->frames = 0;
+    F.tile_order = ls->valid ? (const int *)ls->order.p : nullptr;
+    // costs are measured and re-sorted every kLptPeriod frames (the sort
+    // costs more than a small frame's tail)
+    lpt_sort = !ls->valid || ls->frames % kLptPeriod == 0;
+    F.tile_cost = lpt_sort ? (unsigned *)ls->cost.p : nullptr;
+    ++ls->frames;
+    // the most expensive tiles of the last measurement are split into
+    // quarter-waves (a frame's time is bounded below by its slowest wave);
+    // render_kernel only: 16 lanes must hold whole pixels
+    const bool levels = (ctx->S.bvh4 && F.spp >= 16) || F.max_bounces > rtd::kMaxBounces;  // (or deep: no splits)
+    if (F.tile_order && !count && !levels && kSplitDiv > 0 && 16 % F.spp == 0 && F.num_tiles <= kSplitMaxTiles) {
+        F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
+        // sixteenth-waves (4 lanes) must hold whole pixels too
+        if (kSplit16Div > 0 && 4 % F.spp == 0) {
+            F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / kSplit16Div));
+            F.split_tiles -= F.split16_tiles;
+        }
+    } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
+               F.num_tiles <= kSplit16MaxTiles) {
+        F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
+    }
+    // render_kernel's ray tallies: one plain store per wave into this slot's
+    // buffer, reduced after the launch on the same stream (an atomic per wave
+    // holds the wave's slot for its round trip: C2 -13 %, C3 -4 %)
+    if (!count) {  // render_kernel and render_levels_kernel
+        const size_t bytes = (size_t)rtk::render_mega_waves(F) * sizeof(uint4);
+        if (bytes > ls->wave_counts.cap) {  // a new buffer carries no launch's tag
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->wave_counts, bytes));
+            HIP_OR_FAIL(ctx, hipMemsetAsync(ls->wave_counts.p, 0, ls->wave_counts.cap, ctx->stream));
+        }
+        F.wave_counts = (uint4 *)ls->wave_counts.p;
+        if (++ctx->count_tag == 0) ++ctx->count_tag;
+        F.count_tag = ctx->count_tag;
+    }
+    return RT_OK;
+}
+
+int lpt_sort_now(rt_ctx *ctx, const rtd::FrameDev &F, LptSlot *ls) {
+    HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
+                                             (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
+                                             ls->scratch.p, ls->scratch.cap, ctx->stream));
+    ls->valid = true;
+    return RT_OK;
+}
+
+// The render path a frame takes.
+struct Path {
+    bool count, packet, wavefront, mega;
+};
+
+Path frame_path(const rt_ctx *ctx, const rt_render_params *prm) {
+    Path p;
+    p.count = (prm->flags & RT_FLAG_COUNT_TESTS) != 0;
+    // MaxReflectionBounces beyond the fold stack: only the megakernel's
+    // deep-chain instance folds unbounded chains
+    const bool deep = prm->max_reflection_bounces > rtd::kMaxBounces;
+    p.packet = !deep && (prm->flags & RT_FLAG_PACKET) != 0 && ctx->S.bvh4;  // packets walk 4-wide nodes
+    p.wavefront = !deep && !p.packet && (prm->flags & RT_FLAG_WAVEFRONT) != 0;
+    p.mega = !p.packet && !p.wavefront;  // default
+    return p;
+}
+
+// Enqueues the trace launch(es) of F on the context's stream.
+int launch_frame(rt_ctx *ctx, rtd::FrameDev &F, const Path &P, const rtw::Args &A, int chunk_tiles) {
+    if (P.packet)
+        HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, P.count, ctx->stream));
+    else if (P.mega)
+        HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, P.count, ctx->stream));
+    else if (P.wavefront && F.num_tiles > 0)
+        HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, P.count, ctx->stream));
+    return RT_OK;
+}
+
+int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *d_out, rt_stats *stats,
+              std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes) {
+    Range range("rt_frame");
+    F.out = d_out;
+    F.counters = ctx->d_counters;
+    const Path P = frame_path(ctx, prm);
+    const bool async = (prm->flags & RT_FLAG_ASYNC) != 0;
+    if (async && host_out) return fail(ctx, RT_E_INVALID, "RT_FLAG_ASYNC needs a device output (rt_render_device)");
+    if (!async) {
+        int st = settle_async(ctx);
+        if (st) return st;
+    }
+    int chunk_tiles = 0;
+    rtw::Args A{};
+    if (P.wavefront && F.num_tiles > 0) {
+        int st = prepare_wavefront(ctx, F, chunk_tiles, A);
+        if (st) return st;
+    }
+    // rt_render into a host Color[]: the frame in row slabs, each copied to the
+    // host while the next ones render (the PCIe copy is the longer part)
+    const bool slabs = host_out && out_bytes && F.band_count == 1 && !P.wavefront;
+    struct Launch {
+        rtd::FrameDev F;
+        LptSlot *ls;
+        bool sort;
+        hipStream_t stream;
+        int r0, r1;
+    };
+    std::vector<Launch> launches;
+    const hipStream_t base = ctx->stream;
+    struct Restore {
+        rt_ctx *c;
+        hipStream_t s;
+        ~Restore() { c->stream = s; }
+    } restore{ctx, base};
+    int row_bytes = 0;
+    // every launch's longest-first state first (its first use allocates):
+    // outside the timed region, which covers device work only
+    if (slabs) {
+        row_bytes = (int)(out_bytes / (size_t)std::max(1, F.local_rows));
+        double wts[kMaxSlabs];
+        for (int k = 0; k < kMaxSlabs; ++k) wts[k] = 1.0;
+        const bool copy_bound = F.out_format == rtd::kOutFloat4 || F.out_format == rtd::kOutRGB32F;
+        const double *w0 = copy_bound ? kSlabsCopyBound : kSlabsRenderBound;
+        int nslab = out_bytes < kSlabMinFrame ? 1 : copy_bound ? 6 : 4;
+        if (nslab > 1)
+            for (int k = 0; k < nslab; ++k) wts[k] = w0[k];
+#ifdef RT_EXP_SLAB_WEIGHTS
+        {  // measuring builds: -DRT_EXP_SLAB_WEIGHTS=1,1,2,4,8 (relative slab rows)
+            constexpr double w[] = {RT_EXP_SLAB_WEIGHTS};
+            nslab = std::min(kMaxSlabs, (int)(sizeof w / sizeof w[0]));
+            for (int k = 0; k < nslab; ++k) wts[k] = w[k];
+        }
+#endif
+        double cum[kMaxSlabs + 1];
+        cum[0] = 0.0;
+        for (int k = 0; k < nslab; ++k) cum[k + 1] = cum[k] + wts[k];
+        // slab boundaries on whole tile rows
+        const int tile_rows = (F.local_rows + F.tile_h - 1) / F.tile_h;
+        auto bound = [&](int k) {
+            return std::min(F.local_rows, (int)std::lround((double)tile_rows * cum[k] / cum[nslab]) * F.tile_h);
+        };
+        if (!ctx->copy_stream) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+        while ((int)ctx->slab_done.size() < nslab) {
+            hipEvent_t e;
+            HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            ctx->slab_done.push_back(e);
+        }
+        // slabs alternate between two streams, so a slab's tail overlaps the
+        // next slab instead of idling the GPU
+        if (!ctx->slab_stream2) HIP_OR_FAIL(ctx, hipStreamCreateWithFlags(&ctx->slab_stream2, hipStreamNonBlocking));
+        for (int k = 0; k < nslab; ++k) {
+            Launch L{};
+            L.stream = ctx->stream = (k & 1) ? ctx->slab_stream2 : base;
+            L.r0 = bound(k);
+            L.r1 = k + 1 == nslab ? F.local_rows : bound(k + 1);
+            L.F = F;
+            L.F.row0 = L.r0;
+            L.F.local_rows = L.r1 - L.r0;
+            L.F.num_tiles = L.F.res_x > 0 ? L.F.tiles_x * ((L.F.local_rows + L.F.tile_h - 1) / L.F.tile_h) : 0;
+            L.F.out = (char *)d_out + (size_t)L.r0 * row_bytes;
+            int st = lpt_prepare(ctx, L.F, prm, P.mega, P.count, k, L.ls, L.sort);
+            if (st) return st;
+            launches.push_back(L);
+        }
+        ctx->stream = base;
+    } else {
+        // megakernel frames dispatch a previous frame's most expensive tiles
+        // first (a frame's tail is its slowest tiles); the order is kept per stream
+        Launch L{};
+        L.F = F;
+        L.stream = base;
+        int st = lpt_prepare(ctx, L.F, prm, P.mega, P.count, 0, L.ls, L.sort);
+        if (st) return st;
+        launches.push_back(L);
+    }
+    const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
+    if (!async || ctx->async_frames == 0) {
+        // async frames share one set of counters until rt_finish / the next synchronous frame
+        HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->d_counters, 0, ctr_bytes, ctx->stream));
+        HIP_OR_FAIL(ctx, hipEventRecord(async ? ctx->ev_a0 : ctx->ev0, ctx->stream));
+    } else {
+        // a later async frame may be on another stream (rt_set_stream between
+        // frames): it must not count before the counters were zeroed
+        HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_a0, 0));
+    }
+    if (slabs) {
+        const int nslab = (int)launches.size();
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev_slab0, base));
+        HIP_OR_FAIL(ctx, hipStreamWaitEvent(ctx->slab_stream2, ctx->ev_slab0, 0));
+        if (!ctx->copier.th.joinable()) ctx->copier.start(ctx->device, ctx->copy_stream);
+        // once a copy is posted, every return waits for the posted copies:
+        // the copier must never write into the caller's buffer after
+        // rt_render has returned (an error return included), nor leave an
+        // error behind for the next frame's wait
+        struct Drain {
+            Copier *c = nullptr;
+            ~Drain() {
+                if (c) (void)c->wait();
+            }
+        } drain;
+        for (int k = 0; k < nslab; ++k) {
+            ctx->stream = launches[k].stream;
+            if (k == ctx->debug_fail_slab)  // rt_debug_set(RT_DEBUG_FAIL_SLAB): tests only
+                return fail(ctx, RT_E_INTERNAL, "injected failure before slab %d (RT_DEBUG_FAIL_SLAB)", k);
+            int st = launch_frame(ctx, launches[k].F, P, A, chunk_tiles);
+            if (st) return st;
+            HIP_OR_FAIL(ctx, hipEventRecord(ctx->slab_done[k], ctx->stream));
+            // the copier thread copies slab k once its launch has ended, while
+            // this thread enqueues the next launches
+            const int r0 = launches[k].r0, r1 = launches[k].r1;
+            if (r1 > r0) {
+                ctx->copier.post({ctx->slab_done[k], (char *)host_out + (size_t)r0 * row_bytes,
+                                  (const char *)d_out + (size_t)r0 * row_bytes, (size_t)(r1 - r0) * row_bytes});
+                drain.c = &ctx->copier;
+            }
+        }
+        ctx->stream = base;
+        if (nslab > 1) HIP_OR_FAIL(ctx, hipStreamWaitEvent(base, ctx->slab_done[nslab - (nslab & 1 ? 2 : 1)], 0));
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, base));
+        for (Launch &L : launches) {  // after the timed region: the order of the next frames
+            if (!L.sort) continue;
+            ctx->stream = L.stream;
+            int st = lpt_sort_now(ctx, L.F, L.ls);
+            if (st) return st;
+        }
+        ctx->stream = base;
+        int st = fold_counters(ctx, base);  // base has waited for every launch
+        if (st) return st;
+        drain.c = nullptr;
+        HIP_OR_FAIL(ctx, ctx->copier.wait());  // every slab is in the caller's buffer
+    } else {
+        Launch &L = launches[0];
+        int st = launch_frame(ctx, L.F, P, A, chunk_tiles);
+        if (st) return st;
+        if (async) {
+            if (L.sort) {
+                st = lpt_sort_now(ctx, L.F, L.ls);
+                if (st) return st;
+            }
+            st = record_async_end(ctx);
+            if (st) return st;
+            if (ctx->async_frames++ == 0 && ctx->async_t0_set == false) {
+                ctx->async_t0 = t_start;
+                ctx->async_t0_set = true;
+            }
+            if (stats) std::memset(stats, 0, sizeof *stats);
+            return RT_OK;
+        }
+        HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+        st = fold_counters(ctx, ctx->stream);
+        if (st) return st;
+        if (L.sort) {  // after the timed region: the order of the next frames
+            st = lpt_sort_now(ctx, L.F, L.ls);
+            if (st) return st;
+        }
+        if (host_out && out_bytes)
+            HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long counts[rtd::kCounterWords];
+    read_folded(ctx, counts);
+    if (stats) {
+        float ms = 0.0f;
+        HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        fill_stats(stats, counts, ms,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+    }
+    return RT_OK;
+}
+
+}  // namespace rti

@@ -83,7 +83,8 @@ struct RefitArgs {
     const int *internal_children;   // per node
     int *arrivals;                  // per node, zeroed by refit_tree
     int empty_ref;                  // the unused slots' ref (+inf boxes, left alone)
-    float *quality;                 // [0] sum of internal slots' half areas, [1] root half area (zeroed)
+    float *quality;                 // [0] sum of internal slots' half areas, [1] root half area; [2..3]: the
+                                    // sum's 64-bit fixed-point accumulator (16 B, zeroed by refit_tree)
 };
 
 hipError_t refit_tree(const RefitArgs &a, hipStream_t stream);

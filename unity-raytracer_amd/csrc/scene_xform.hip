@@ -231,9 +231,22 @@ __device__ __forceinline__ float half_area3(float4 lo, float4 hi) {
     return dx * dy + dy * dz + dz * dx;
 }
 
+// The tree-quality sum (RefitArgs::quality) in fixed point: each internal
+// slot's half area in units of 2^-24 of the scene box's, added as a 64-bit
+// integer — an order-free, hence reproducible, sum (a float atomic sum in
+// arrival order could flip the rebuild decision from run to run).  0 when
+// the scene box is degenerate or not finite (the root then reports NaN).
+__device__ __forceinline__ double quality_scale(const float *box) {
+    const double dx = (double)box[3] - box[0], dy = (double)box[4] - box[1], dz = (double)box[5] - box[2];
+    const double sa = dx * dy + dy * dz + dz * dx;
+    return sa > 1e-30 && sa < 1e30 ? 0x1p24 / sa : 0.0;
+}
+
 __global__ void k_refit_nodes(RefitArgs a) {
     int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= a.nnodes || a.internal_children[v] != 0) return;
+    const double qscale = quality_scale(a.box);
+    unsigned long long *const qsum = reinterpret_cast<unsigned long long *>(a.quality + 2);
     for (;;) {
         rtd::BvhNode4 *nd = a.nodes + v;
         const int4 ch = nd->child;
@@ -268,9 +281,12 @@ __global__ void k_refit_nodes(RefitArgs a) {
             ulo = make_float4(fminf(ulo.x, lo.x), fminf(ulo.y, lo.y), fminf(ulo.z, lo.z), 0.0f);
             uhi = make_float4(fmaxf(uhi.x, hi.x), fmaxf(uhi.y, hi.y), fmaxf(uhi.z, hi.z), 0.0f);
         }
-        if (inner_area > 0.0f) atomicAdd(a.quality, inner_area);
+        if (inner_area > 0.0f && qscale > 0.0)  // one term < 2^34, at most 2^27 nodes: no overflow
+            atomicAdd(qsum, __double2ull_rn(fmin((double)inner_area * qscale, 0x1p34)));
         const int ps = a.parent_slot[v];
-        if (ps < 0) {
+        if (ps < 0) {  // the root: every other node's term was added before its arrival count
+            const unsigned long long sum = __hip_atomic_load(qsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.quality[0] = qscale > 0.0 ? (float)((double)sum / qscale) : __int_as_float(0x7fc00000);
             a.quality[1] = half_area3(ulo, uhi);
             return;
         }
@@ -317,7 +333,7 @@ hipError_t refit_links(const RefitArgs &a, int *parent_slot, int *internal_child
 hipError_t refit_tree(const RefitArgs &a, hipStream_t stream) {
     if (a.nnodes <= 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(a.arrivals, 0, sizeof(int) * (size_t)a.nnodes, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(a.quality, 0, 2 * sizeof(float), stream);
+    if (e == hipSuccess) e = hipMemsetAsync(a.quality, 0, 4 * sizeof(float), stream);
     if (e != hipSuccess) return e;
     const int np = a.ntri + a.nsph;
     if (np > 0) hipLaunchKernelGGL(k_refit_prims, dim3((np + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, a);

@@ -217,13 +217,35 @@ __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, 
     }
 }
 
+// tile -> (tx, ty) = (tile % tiles_x, tile / tiles_x) by the per-frame magic
+// multiplier (FrameDev::tiles_x_magic = floor(2^32 / tiles_x)): the estimate
+// is the quotient or one less, fixed by one compare — a few scalar
+// instructions instead of an integer-division sequence on the tile's critical
+// path.  Exact for every non-negative 32-bit tile.
+__device__ __forceinline__ void tile_xy(const rtd::FrameDev &F, int tile, int &tx, int &ty) {
+#ifdef RT_EXP_LEAN
+    unsigned q = __umulhi((unsigned)tile, F.tiles_x_magic);
+    int r = tile - (int)q * F.tiles_x;
+    if (r >= F.tiles_x) {
+        ++q;
+        r -= F.tiles_x;
+    }
+    tx = r;
+    ty = (int)q;
+#else
+    ty = tile / F.tiles_x;
+    tx = tile - ty * F.tiles_x;
+#endif
+}
+
 // The pixel rectangle of a tile (image rows; tile index wave-uniform) for the
 // camera packet's frustum start (packet.h cut_start).  Valid when a tile's
 // rows lie in one band block (rt_abi.cpp cut_setup checks band_rows).
 template <bool Q4 = false>
 __device__ __forceinline__ rtp::TileRect tile_rect(const rtd::FrameDev &F, int tile) {
     const int tw = Q4 ? 4 : F.tile_w, th = Q4 ? 4 : F.tile_h;
-    const int ty = tile / F.tiles_x, tx = tile - ty * F.tiles_x;
+    int tx, ty;
+    tile_xy(F, tile, tx, ty);
     const int ly = ty * th;
     int gy = ly + F.row0;
     if (F.band_count > 1) {
@@ -243,7 +265,8 @@ __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int
     const int pix = lp;
     s = Q4 ? lane & 3 : lane - lp * spp;
     const int tw = Q4 ? 4 : F.tile_w, th = Q4 ? 4 : F.tile_h;
-    const int tx = tile % F.tiles_x, ty = tile / F.tiles_x;
+    int tx, ty;
+    tile_xy(F, tile, tx, ty);
     px = tx * tw + (Q4 ? pix & 3 : pix % tw);
     ly = ty * th + (Q4 ? pix >> 2 : pix / tw);
     gy = ly + F.row0;

@@ -213,8 +213,9 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 // The counting launch keeps the per-ray traversal's canonical counts.
 template <bool COUNT, bool DEEP>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
-                                         int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs) {
+                                         int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs, int tile) {
     (void)sg;
+    (void)tile;
     if (COUNT || !S.bvh4) return shade_levels<COUNT, DEEP>(S, F, o, d, 0, st, cnt);
     RT_SEG(const unsigned long long tq0 = __builtin_amdgcn_s_memtime();)
     rtt::RayCtx r;
@@ -224,6 +225,12 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     RT_SEG(sg.visits += P.nodes + ((unsigned long long)P.leaves << 32);
            const unsigned long long tq1 = __builtin_amdgcn_s_memtime(); sg.setup = tq0; sg.prim = tq1 - tq0;)
     if (P.best_rank < 0) return rtt::ld3(F.bg255);  // :310-311
+#ifdef RT_EXP_LASTOCC
+    // this tile's occluder hints of the last frame (one per light, < kHintLights)
+    int *const hints = F.shadow_hint ? F.shadow_hint + (size_t)tile * kHintLights : nullptr;
+    int4 hv = make_int4(0, 0, 0, 0);
+    if (hints) hv = rtt::cload(reinterpret_cast<const int4 *>(hints));
+#endif
     const rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
@@ -237,7 +244,14 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         rtt::setup_ray(rs, sr.o, sr.dir);
         rtp::PacketLane Q;
         RT_SEG(const unsigned long long tw0 = __builtin_amdgcn_s_memtime();)
+#ifdef RT_EXP_LASTOCC
+        const bool hl = hints && l < kHintLights;
+        const int h = !hl ? 0 : l == 0 ? hv.x : l == 1 ? hv.y : l == 2 ? hv.z : hv.w;
+        rtp::packet_trace<true, COUNT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr, h,
+                                       hl ? hints + l : nullptr);
+#else
         rtp::packet_trace<true, COUNT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
+#endif
         RT_SEG(sg.shadow += __builtin_amdgcn_s_memtime() - tw0;
                sg.visits += Q.nodes + ((unsigned long long)Q.leaves << 32);)
         if (moot || Q.best_rank == 1) continue;
@@ -276,6 +290,11 @@ template <bool COUNT, bool DEEP, bool Q4>
 __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
                                             SegClock &sg) {
+#ifdef RT_EXP_LEAN
+    // the cut entries do not depend on the tile: their loads are issued first
+    rtp::CutLane cl;
+    if (!COUNT) cl = rtp::cut_load(S);
+#endif
     int px, ly, gy, s;
     const bool active =
         rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
@@ -288,7 +307,11 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
 #endif
     // the camera packet's start below the top-level cut (every lane active here)
     rtp::CutStart cs = {0, 0, 0, -1};
+#ifdef RT_EXP_LEAN
+    if (!COUNT && !sky && F.cut_test) cs = rtp::cut_select(S, F, rts::tile_rect<Q4>(F, tile), wstack, &cl);
+#else
     if (!COUNT && !sky && F.cut_test) cs = rtp::cut_select(S, F, rts::tile_rect<Q4>(F, tile), wstack);
+#endif
     if (active) {
         if (COUNT) cnt.primary += 1;  // otherwise F.primary_total, added once per launch
         if (sky) {
@@ -302,7 +325,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
                 cnt.scene_miss +=
                     !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
             }
-            color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg, cs);
+            color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg, cs, tile);
         }
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
@@ -751,9 +774,9 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
                                      F.spp);
     int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
 #ifdef RT_EXP_DROP_TAIL
-    // measurement only: the last N waves of the longest-first order (the sky
-    // tiles) are not launched (their pixels are left as they were)
-    if (const char *e = getenv("RT_EXP_DROP_TAIL")) blocks = blocks > atoi(e) ? blocks - atoi(e) : 0;
+    // measurement only: the last RT_EXP_DROP_TAIL waves of the longest-first
+    // order (the sky tiles) are not launched (their pixels are left as they were)
+    blocks = blocks > RT_EXP_DROP_TAIL ? blocks - RT_EXP_DROP_TAIL : 0;
 #endif
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
@@ -780,7 +803,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
-        const int waves = blocks * kMkWaves;
+        const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
                            (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
     }

@@ -269,6 +269,23 @@ __device__ __forceinline__ float child_key(float lx, float hx, float ly, float h
     return tn <= tf ? tn : INFINITY;
 }
 
+// child_key in exact arithmetic, (plane - o) * (1.0f / d) rounded per IEEE
+// operation: the node test of the counting launch (RT_FLAG_COUNT_TESTS), whose
+// box/triangle/sphere counts are the canonical per-frame counts SURVEY §8(d)
+// prices — the CPU oracle's traversal of the same exported tree computes the
+// identical values (oracle/rt_oracle.c bvh4_query), so the two walks visit
+// the same nodes in the same order and their counts must agree exactly.
+__device__ __forceinline__ float child_key_exact(float lx, float hx, float ly, float hy, float lz, float hz,
+                                                 const RayCtx &r, float tcull) {
+    const f3 o = r.o, iv = r.inv();
+    const float ax = (lx - o.x) * iv.x, bx = (hx - o.x) * iv.x;
+    const float ay = (ly - o.y) * iv.y, by = (hy - o.y) * iv.y;
+    const float az = (lz - o.z) * iv.z, bz = (hz - o.z) * iv.z;
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), tcull));
+    return tn <= tf ? tn : INFINITY;
+}
+
 // child_key with the near/far planes already chosen by the ray's direction
 // signs (near = lo for a positive inverse direction): max/min of the same
 // plane distances, so the same result in fewer instructions.
@@ -309,10 +326,18 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         const rtd::BvhNode4 *np = S.nodes4 + t.node;
         const float4 lx = np->lox, hx = np->hix, ly = np->loy, hy = np->hiy, lz = np->loz, hz = np->hiz;
         const int4 ch = np->child;
-        float k0 = child_key(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, t.tcull);
-        float k1 = child_key(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, t.tcull);
-        float k2 = child_key(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, t.tcull);
-        float k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, t.tcull);
+        float k0, k1, k2, k3;
+        if (COUNT) {  // the canonical counts' exact node test (child_key_exact)
+            k0 = child_key_exact(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, t.tcull);
+            k1 = child_key_exact(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, t.tcull);
+            k2 = child_key_exact(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, t.tcull);
+            k3 = child_key_exact(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, t.tcull);
+        } else {
+            k0 = child_key(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, t.tcull);
+            k1 = child_key(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, t.tcull);
+            k2 = child_key(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, t.tcull);
+            k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, t.tcull);
+        }
         if (COUNT) cnt.box += 4;
         int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
         RT_CSWAP(0, 1);  // sort the four keys (5 compare-swaps)
