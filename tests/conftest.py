@@ -21,7 +21,13 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def rt():
-    return _rt_pkg.load()
+    mod = _rt_pkg.load()
+    # measuring sessions only: run the suite against a library variant
+    # (unity-raytracer_amd/lib/variants/<name>/librt_mi355.so)
+    v = os.environ.get("RT_TEST_LIB_VARIANT")
+    if v:
+        mod.abi.LIB_PATH = os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", v, "librt_mi355.so")
+    return mod
 
 
 @pytest.fixture(scope="session")

@@ -77,3 +77,42 @@ def test_host_frames_repeat_and_move(gpu_ctx, rt):
             gpu_ctx.render_device(cam, fr.plane, p, dev.data_ptr(), host.nbytes)
             ref = dev.cpu().numpy().view(np.uint32).reshape(host.shape)
             assert np.array_equal(host.view(np.uint32), ref), i
+
+
+@pytest.mark.parametrize("fail_slab", [1, 3, 5])
+def test_failed_slab_leaves_no_copy_behind(gpu_ctx, rt, fail_slab):
+    """An error in a later slab (rt_debug_set RT_DEBUG_FAIL_SLAB injects one
+    before that slab's launch) must not return before the copies already
+    posted for the earlier slabs have finished: the caller may free or reuse
+    its Color[] at once.  The earlier slabs' rows are the frame's, the rest
+    of the buffer is untouched, nothing changes after the return, and the
+    next frame succeeds with no error left behind."""
+    import ctypes as C
+    import time
+
+    fr = rt.make("C3")  # float RGBA 1080p: six row slabs
+    gpu_ctx.set_scene(fr.scene)
+    p = rt.frame_params(fr)
+    good, _ = gpu_ctx.render(fr.camera, fr.plane, p)
+    lib = gpu_ctx.lib
+    assert lib.rt_debug_set(gpu_ctx.h, rt.abi.RT_DEBUG_FAIL_SLAB, fail_slab) == 0
+    try:
+        buf = np.full(good.shape, -7.0, np.float32)
+        stats = rt.abi.rt_stats()
+        cam, pl = rt.raytracing.camera_struct(fr.camera), rt.raytracing.plane_struct(fr.plane)
+        st = lib.rt_render(gpu_ctx.h, C.byref(cam), C.byref(pl), C.byref(p), buf.ctypes.data_as(C.c_void_p),
+                           C.byref(stats))
+        assert st == rt.abi.RT_E_INTERNAL
+        assert b"slab" in lib.rt_last_error(gpu_ctx.h)
+        snap = buf.copy()
+        time.sleep(0.2)  # a copy still in flight would land now
+        assert np.array_equal(snap.view(np.uint32), buf.view(np.uint32))
+        done = np.all(buf == good, axis=(1, 2))      # rows the finished slabs copied
+        untouched = np.all(buf == -7.0, axis=(1, 2))  # rows of the slabs never launched
+        assert np.all(done | untouched)
+        first_bad = int(np.argmin(done)) if not done.all() else len(done)
+        assert 0 < first_bad < len(done) and untouched[first_bad:].all()
+    finally:
+        assert lib.rt_debug_set(gpu_ctx.h, rt.abi.RT_DEBUG_FAIL_SLAB, -1) == 0
+    again, _ = gpu_ctx.render(fr.camera, fr.plane, p)
+    assert np.array_equal(again.view(np.uint32), good.view(np.uint32))

@@ -1,6 +1,7 @@
 # PMC passes for one config's trace kernel (one counter group per rocprofv3
 # run, --kernel-trace only alongside; MI355X_MICROARCH.md "rocprofv3 PMC slots").
-# usage (on the GPU box): bash tools/pmc_round.sh <tag> [config] [bands]
+# usage (on the GPU box): [VARIANT=name] bash tools/pmc_round.sh <tag> [config] [bands]
+#   VARIANT: measure lib/variants/<name>/librt_mi355.so instead of the default build
 #   config: C3 (default) / C2 / C4 / C5; bands: 1 (whole frame, default) or N
 #   (row band 0 of N: one rank's share of an N-GPU frame).
 # Writes gpurun_out/pmc_<tag>_<config>[_b<N>]/summary.json; copy it to
@@ -19,10 +20,11 @@ rows = fr.plane.ResolutionY if $bands == 1 else -(-fr.plane.ResolutionY // (8 * 
 print(bench.trace_kernel_name('megakernel', fr.spp, fr.max_bounces, fr.plane.ResolutionX, rows))") || exit 1
 # the split instance needs a measured tile order: probe renders the timed frames after two warm ones
 frames=3
-out=$R/gpurun_out/pmc_${tag}_$sfx
+out=$R/gpurun_out/pmc_${tag}_$sfx${VARIANT:+_$VARIANT}
 run() {
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $2 --output-format csv -d $out/$1 -o run -- \
-    python3 $R/tools/probe.py --config $cfg --modes megakernel --frames $frames $band_arg > $out/$1.log 2>&1
+    python3 $R/tools/probe.py --config $cfg --modes megakernel --frames $frames --variants ${VARIANT:-default} \
+      $band_arg > $out/$1.log 2>&1
 }
 mkdir -p $out
 echo "pmc $cfg bands $bands kernel '$kernel'"

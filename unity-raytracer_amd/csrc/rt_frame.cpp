@@ -411,6 +411,19 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
                F.num_tiles <= kSplit16MaxTiles) {
         F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
     }
+#ifdef RT_EXP_SKYPASS
+    // the sky pre-pass (trace.hip sky_pass_kernel): unsplit render_kernel frames with the sky test on
+    if (!count && !levels && F.split_tiles == 0 && F.split16_tiles == 0 && F.sky_test) {
+        const size_t wb = (size_t)F.num_tiles * sizeof(int);
+        if (wb > ls->work.cap) HIP_OR_FAIL(ctx, ensure(ctx, ls->work, wb));
+        if (!ls->work_count.p) {
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->work_count, sizeof(unsigned)));
+            HIP_OR_FAIL(ctx, hipMemsetAsync(ls->work_count.p, 0, sizeof(unsigned), ctx->stream));
+        }
+        F.work = (int *)ls->work.p;
+        F.work_count = (unsigned *)ls->work_count.p;
+    }
+#endif
     // render_kernel's ray tallies: one plain store per wave into this slot's
     // buffer, reduced after the launch on the same stream (an atomic per wave
     // holds the wave's slot for its round trip: C2 -13 %, C3 -4 %)

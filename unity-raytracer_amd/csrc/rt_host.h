@@ -77,12 +77,13 @@ struct LptSlot {
     GrowBuf cost, cost_sorted, iota, order, scratch;
     GrowBuf wave_counts;  // render_kernel's per-wave ray tallies (rtd::FrameDev::wave_counts)
     GrowBuf hints;        // render_kernel's shadow-packet occluder hints (rtd::FrameDev::shadow_hint)
+    GrowBuf work, work_count;  // the sky pre-pass's tile list and its length (rtd::FrameDev::work)
     long long key = -1;
     unsigned long long scene = ~0ull;
     bool valid = false;
     long long frames = 0;
     void release() {
-        for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch, &wave_counts, &hints}) {
+        for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch, &wave_counts, &hints, &work, &work_count}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;

@@ -289,7 +289,7 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 template <bool COUNT, bool DEEP, bool Q4>
 __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
-                                            SegClock &sg) {
+                                            SegClock &sg, bool sky_done = false) {
 #ifdef RT_EXP_LEAN
     // the cut entries do not depend on the tile: their loads are issued first
     rtp::CutLane cl;
@@ -303,7 +303,8 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     // without its exact rays (shade.h sky_maybe; the counting launch traces all)
     bool sky = false;
 #ifndef RT_EXP_NOSKY
-    if (!COUNT) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4>(F, px, gy, s))) == 0;
+    // (sky_done: the sky pre-pass has answered this frame's sky tiles already)
+    if (!COUNT && !sky_done) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4>(F, px, gy, s))) == 0;
 #endif
     // the camera packet's start below the top-level cut (every lane active here)
     rtp::CutStart cs = {0, 0, 0, -1};
@@ -391,7 +392,19 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     // the tile index is wave-uniform and kept in an SGPR: the slot -> pixel
     // integer math runs on the scalar unit and nothing of it is spilled
     int tile = idx;
+#ifdef RT_EXP_SKYPASS
+    // after the sky pre-pass: only the tiles it left, in dispatch order
+    const bool sky_done = !COUNT && !SPLIT && F.work;
+    if (sky_done) {
+        if (wid >= (int)rtt::cload(F.work_count)) return;  // wave-uniform
+        tile = rtt::cload(F.work + wid);
+    } else if (F.tile_order) {
+        tile = rtt::cload(F.tile_order + idx);
+    }
+#else
+    const bool sky_done = false;
     if (F.tile_order) tile = rtt::cload(F.tile_order + idx);
+#endif
     tile = __builtin_amdgcn_readfirstlane(tile);
     // the launch's camera samples (one per active lane of every tile, computed
     // by the host: rt_device.h active_samples), counted once per launch
@@ -399,7 +412,7 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    const bool sky = render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    const bool sky = render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, sky_done);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
@@ -460,7 +473,9 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
 // launch never does).
 __global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n, unsigned tag,
                                                          unsigned long long primary_total,
-                                                         unsigned long long *counters) {
+                                                         unsigned long long *counters, unsigned *work_count) {
+    // the sky pre-pass's counter, for the next frame (the launch that read it has ended)
+    if (work_count && blockIdx.x == 0 && threadIdx.x == 0) *work_count = 0u;
     unsigned long long sh = 0, rf = 0, mo = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const uint4 v = wc[i];
@@ -492,6 +507,55 @@ __global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n
         if (b) atomicAdd(ctr + 2, b);
         if (c) atomicAdd(ctr + 8, c);
     }
+}
+
+// Sky pre-pass (frames whose tiles render_kernel dispatches unsplit, sky test
+// on): one thread per tile in dispatch order runs the same per-sample test as
+// render_tile (shade.h sky_maybe, every slot of the tile) and answers a sky
+// tile at once — the background, summed and scaled exactly as render_tile
+// sums a sky wave's samples, stored for each of its pixels
+// (RayTracingSetup.cs:310-311) — and records a zero cost key; the other tiles
+// are appended to F.work (one atomic per wave, the wave's order kept), which
+// render_kernel then dispatches instead of the whole frame.  The heavy
+// megakernel waves (96 VGPRs, LDS stacks) are spent on tiles with rays only.
+template <bool Q4>
+__global__ __launch_bounds__(256) void sky_pass_kernel(SceneDev S, FrameDev F) {
+    (void)S;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    bool keep = false;
+    int tile = 0;
+    if (idx < F.num_tiles) {
+        tile = F.tile_order ? F.tile_order[idx] : idx;
+        bool maybe = false;
+        for (int j = 0; j < kWaveSize && !maybe; ++j) {
+            int px, ly, gy, s;
+            if (rts::slot_pixel<Q4>(F, tile, j, px, ly, gy, s) && rts::sky_maybe<Q4>(F, px, gy, s)) maybe = true;
+        }
+        keep = maybe;
+        if (!maybe) {
+            const f3 c = rtt::ld3(F.bg255);
+            const int spp = Q4 ? 4 : F.spp;
+            f3 sum = c;  // sample_sum's order: ((s0 + s1) + s2) + ...
+            for (int k = 1; k < spp; ++k) sum = sum + c;
+            f3 v = sum;
+            if (Q4)
+                v = v * 0.25f;
+            else if (spp > 1)
+                v = (spp & (spp - 1)) == 0 ? v * F.inv_spp : v / (float)spp;
+            for (int j = 0; j < kWaveSize; j += spp) {
+                int px, ly, gy, s;
+                if (rts::slot_pixel<Q4>(F, tile, j, px, ly, gy, s)) rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+            }
+            if (F.tile_cost) F.tile_cost[tile] = 0u;
+        }
+    }
+    const unsigned long long m = __ballot(keep);
+    if (m == 0) return;
+    unsigned base = 0;
+    const int lane = threadIdx.x & 63;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(F.work_count, (unsigned)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (keep) F.work[base + __popcll(m & ((1ull << lane) - 1))] = tile;
 }
 
 // The frame's sharded counters summed into kCounterWords words (out: the
@@ -795,17 +859,22 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         if (e != hipSuccess || !F.wave_counts) return e;
         const int waves = F.num_tiles;  // one wave per tile, no splits
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
-                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
+                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters,
+                           F.work_count);
         return hipGetLastError();
     }
-    else if (q4)
+    else if (q4) {
+        if (F.work) hipLaunchKernelGGL(sky_pass_kernel<true>, dim3((F.num_tiles + 255) / 256), dim3(256), 0, stream, S, F);
         hipLaunchKernelGGL((render_kernel<false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    else
+    } else {
+        if (F.work) hipLaunchKernelGGL(sky_pass_kernel<false>, dim3((F.num_tiles + 255) / 256), dim3(256), 0, stream, S, F);
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+    }
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
-                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
+                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters,
+                           F.work_count);
     }
     return hipGetLastError();
 }

@@ -28,7 +28,11 @@ namespace {
 // frames in flight against 7; C5 (64 spp, depth 16) 6 waves +2 %, 5 waves
 // +6 %.
 constexpr int kLvWavesLowSpp = 6;
+#ifdef RT_EXP_LVHIGH
+constexpr int kLvWavesHighSpp = RT_EXP_LVHIGH;  // measuring builds only
+#else
 constexpr int kLvWavesHighSpp = 7;
+#endif
 
 // Level-synchronous all-packet megakernel (the default non-counting path on
 // a 4-wide BVH): one wave = one tile of 64 samples; the Whitted chain
@@ -46,6 +50,12 @@ constexpr int kLvWavesHighSpp = 7;
 template <int MIN_WAVES>
 __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
+#ifdef RT_EXP_LVSTASH
+    // the lane state that lives across a shadow packet, kept in LDS instead of
+    // registers the packet's own values would spill (volatile: reloaded, so
+    // the register copies die at the store)
+    __shared__ float stash_mem[18 * kWaveSize];
+#endif
     const int lane = threadIdx.x & 63;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x;
@@ -101,13 +111,31 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
             const rts::ShadowRay sr = rts::shadow_ray(sf, Lt);
             if (hit) cnt.shadow++;
             // a moot shadow ray (shade.h same_bits) is not traced
-            const f3 lit = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
+            f3 lit = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
             const bool trace = hit && !rts::same_bits(lit, col);
             cnt.moot += hit && !trace;
             rtt::RayCtx rs;
             rtt::setup_ray(rs, sr.o, sr.dir);
             rtp::PacketLane Q;
+#ifdef RT_EXP_LVSTASH
+            volatile float *vs = stash_mem + rtt::lane_id();
+            {
+                const float v[18] = {col.x, col.y, col.z, lit.x, lit.y, lit.z, sf.p.x, sf.p.y, sf.p.z,
+                                     sf.n.x, sf.n.y, sf.n.z, sf.view.x, sf.view.y, sf.view.z, term.x, term.y, term.z};
+#pragma unroll
+                for (int i = 0; i < 18; ++i) vs[i * kWaveSize] = v[i];
+            }
             rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+            vs = stash_mem + rtt::lane_id();
+            col = mk(vs[0], vs[64], vs[128]);
+            lit = mk(vs[192], vs[256], vs[320]);
+            sf.p = mk(vs[384], vs[448], vs[512]);
+            sf.n = mk(vs[576], vs[640], vs[704]);
+            sf.view = mk(vs[768], vs[832], vs[896]);
+            term = mk(vs[960], vs[1024], vs[1088]);
+#else
+            rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+#endif
             if (trace && Q.best_rank != 1) col = lit;
         }
         bool mirror = false;
