@@ -10,7 +10,11 @@ namespace rtb {
 namespace {
 
 constexpr int kBins = 32;
+#ifdef RT_EXP_SAH_TRAV
+constexpr float kTraversalCost = RT_EXP_SAH_TRAV;  // measuring builds only
+#else
 constexpr float kTraversalCost = 1.0f;  // relative to one primitive test
+#endif
 constexpr float kIntersectCost = 1.0f;
 
 struct Box {

@@ -248,8 +248,11 @@ __device__ __forceinline__ CutStart cut_select(const rtd::SceneDev &S, const rtd
 // the most lanes of this tile's shadow packet last time; the walk from the
 // root then never visits it again (each live lane has tested it already, and
 // any-hit order cannot change an answer).  hint_out: where the leaf that
-// retires the most lanes this time is stored (0: none), by one lane.
-template <bool ANY, bool COUNT>
+// retires the most lanes this time is stored (0: none), by one lane.  HINT:
+// compiled only into the split-tile instance of render_kernel (small shards
+// and synchronous frames, whose time is their slowest waves: a 1/8 C3 shard
+// -3 %); in the whole-frame instance the extra scalar state cost 4 % (r04a).
+template <bool ANY, bool COUNT, bool HINT = false>
 __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCtx &r, bool part, float tlimit,
                                              float d2, PacketLane &L, int *wstack, Counts &cnt,
                                              const CutStart *cs = nullptr, int hint = 0, int *hint_out = nullptr) {
@@ -320,15 +323,14 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             if (gate >= 0) wgate = -2;  // the lanes' caches moved on their own
         }
     };
-#ifdef RT_EXP_LASTOCC
     // any-hit: the leaf that retires the most lanes (the next frame's hint)
     int best_leaf = 0, best_retired = 0;  // wave-uniform
     int skip = 0;                         // the hinted leaf, never visited again
     auto note_hint = [&]() {
-        if (!ANY || !hint_out) return;
+        if (!ANY || !HINT || !hint_out) return;
         if (rtt::lane_id() == __ffsll((long long)__ballot(1)) - 1) *hint_out = best_leaf;
     };
-    if (ANY && hint < 0) {
+    if (ANY && HINT && hint < 0) {
         const unsigned long long before = __ballot(L.live);
         visit_leaf(hint);
         const unsigned long long after = __ballot(L.live);
@@ -340,7 +342,6 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
         }
         skip = hint;
     }
-#endif
     while (true) {
         if (!ANY && node >= kCutMark) {
             // a waiting cut entry (cut_select): visited only if a live lane's
@@ -395,15 +396,10 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                 // any-hit (shadow rays): the order cannot change the answer,
                 // so the children any live lane needs are taken in slot order
                 // without the wave-wide sort (C3 -6 %, C2 -3 %, C5 +-0)
-#ifdef RT_EXP_LASTOCC
-                const bool n0 = __ballot(k0 != INFINITY) != 0 && ch.x != skip,
-                           n1 = __ballot(k1 != INFINITY) != 0 && ch.y != skip,
-                           n2 = __ballot(k2 != INFINITY) != 0 && ch.z != skip,
-                           n3 = __ballot(k3 != INFINITY) != 0 && ch.w != skip;
-#else
-                const bool n0 = __ballot(k0 != INFINITY) != 0, n1 = __ballot(k1 != INFINITY) != 0,
-                           n2 = __ballot(k2 != INFINITY) != 0, n3 = __ballot(k3 != INFINITY) != 0;
-#endif
+                const bool n0 = __ballot(k0 != INFINITY) != 0 && (!HINT || ch.x != skip),
+                           n1 = __ballot(k1 != INFINITY) != 0 && (!HINT || ch.y != skip),
+                           n2 = __ballot(k2 != INFINITY) != 0 && (!HINT || ch.z != skip),
+                           n3 = __ballot(k3 != INFINITY) != 0 && (!HINT || ch.w != skip);
                 int nn = 0, nxt = 0;
                 if (n3) { nxt = ch.w; ++nn; }
                 if (n2) { if (nn) RT_PK_PUSH(nxt); nxt = ch.z; ++nn; }
@@ -450,30 +446,25 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             }
             }
         } else {
-#ifdef RT_EXP_LASTOCC
-            const unsigned long long before = ANY ? __ballot(L.live) : 0ull;
+            const unsigned long long before = ANY && HINT ? __ballot(L.live) : 0ull;
             visit_leaf(node);
             if (ANY) {
                 const unsigned long long after = __ballot(L.live);
-                const int retired = __popcll(before & ~after);
-                if (retired > best_retired) {
-                    best_retired = retired;
-                    best_leaf = node;
+                if (HINT) {
+                    const int retired = __popcll(before & ~after);
+                    if (retired > best_retired) {
+                        best_retired = retired;
+                        best_leaf = node;
+                    }
                 }
                 if (after == 0) {
                     note_hint();
                     return;
                 }
             }
-#else
-            visit_leaf(node);
-            if (ANY && __ballot(L.live) == 0) return;
-#endif
         }
         if (sp == 0) {
-#ifdef RT_EXP_LASTOCC
             note_hint();
-#endif
             return;
         }
         --sp;

@@ -215,9 +215,6 @@ struct FrameDev {
     int tile_w, tile_h;      // pixels of one wave's tile
     int tiles_x, num_tiles;
     unsigned tiles_x_magic;  // floor(2^32 / tiles_x) (0xffffffff for 1): tile -> (tx, ty) without a division
-    int *work;               // sky pre-pass (trace.hip sky_pass_kernel): the tiles left after it, in dispatch
-                             // order; null: off (render_kernel tests its own tiles for sky)
-    unsigned *work_count;    // ... their number (reset to 0 by wave_counts_kernel after the launch)
     int *shadow_hint;        // render_kernel: per tile x light (< kHintLights) the leaf that occluded the most
                              // lanes of the tile's first shadow packet last time (0: none); null: off
     void *out;               // local_rows x res_x pixels in out_format

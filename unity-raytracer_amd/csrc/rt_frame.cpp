@@ -239,6 +239,10 @@ constexpr int kSplit16MaxTiles = RT_EXP_SPLIT16MAX;  // measuring builds only
 constexpr int kSplit16MaxTiles = 70000;
 #endif
 constexpr int kSplit16DivLarge = 4096;
+// A synchronous frame (no RT_FLAG_ASYNC: Update() waits for it, RayTracingSetup.cs:
+// 171-199) has no next frame to hide its tail behind, so whole frames of any size
+// split their slowest 1/4096 into sixteenth-waves too: C3 single frame -9 % (0.290 ->
+// 0.264 ms, profiles/r04/abx_split); frames in flight keep the 70,000-tile limit.
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
 // kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
@@ -367,28 +371,13 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         ls->key = key;
         ls->valid = false;
     }
-    bool hints_stale = false;
     if (ls->scene != ctx->scene_version) {
         // a new or updated scene (rt_update_mesh_transforms every Update): the
         // last order stays a valid permutation of the tiles and, animation being
         // temporally coherent, a good one — keep dispatching by it and keep the
         // re-sort period (re-sorting after every update cost ~55 us a frame)
         ls->scene = ctx->scene_version;
-        hints_stale = true;  // leaf refs of another tree may lie outside this one's arrays
     }
-#ifdef RT_EXP_LASTOCC
-    {
-        const size_t hb = (size_t)F.num_tiles * rtd::kHintLights * sizeof(int);
-        if (hb > ls->hints.cap) {
-            HIP_OR_FAIL(ctx, ensure(ctx, ls->hints, hb));
-            hints_stale = true;
-        }
-        if (hints_stale) HIP_OR_FAIL(ctx, hipMemsetAsync(ls->hints.p, 0, hb, ctx->stream));
-        F.shadow_hint = count ? nullptr : (int *)ls->hints.p;
-    }
-#else
-    (void)hints_stale;
-#endif
     if (!ls->valid) ls->frames = 0;
     F.tile_order = ls->valid ? (const int *)ls->order.p : nullptr;
     // costs are measured and re-sorted every kLptPeriod frames (the sort
@@ -408,22 +397,24 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
             F.split_tiles -= F.split16_tiles;
         }
     } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
-               F.num_tiles <= kSplit16MaxTiles) {
+               (F.num_tiles <= kSplit16MaxTiles || (prm->flags & RT_FLAG_ASYNC) == 0)) {
         F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
     }
-#ifdef RT_EXP_SKYPASS
-    // the sky pre-pass (trace.hip sky_pass_kernel): unsplit render_kernel frames with the sky test on
-    if (!count && !levels && F.split_tiles == 0 && F.split16_tiles == 0 && F.sky_test) {
-        const size_t wb = (size_t)F.num_tiles * sizeof(int);
-        if (wb > ls->work.cap) HIP_OR_FAIL(ctx, ensure(ctx, ls->work, wb));
-        if (!ls->work_count.p) {
-            HIP_OR_FAIL(ctx, ensure(ctx, ls->work_count, sizeof(unsigned)));
-            HIP_OR_FAIL(ctx, hipMemsetAsync(ls->work_count.p, 0, sizeof(unsigned), ctx->stream));
+    // the split-tile instance's shadow occluder hints (packet.h packet_trace
+    // HINT): leaf refs of the tree they were recorded on, so cleared whenever
+    // the scene changed (another tree's refs may lie outside this one's arrays)
+    if (!count && !levels && (F.split_tiles > 0 || F.split16_tiles > 0)) {
+        const size_t hb = (size_t)F.num_tiles * rtd::kHintLights * sizeof(int);
+        bool clear = ls->hints_scene != ctx->scene_version || ls->hints_key != key;
+        if (hb > ls->hints.cap) {
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->hints, hb));
+            clear = true;
         }
-        F.work = (int *)ls->work.p;
-        F.work_count = (unsigned *)ls->work_count.p;
+        if (clear) HIP_OR_FAIL(ctx, hipMemsetAsync(ls->hints.p, 0, hb, ctx->stream));
+        ls->hints_scene = ctx->scene_version;
+        ls->hints_key = key;
+        F.shadow_hint = (int *)ls->hints.p;
     }
-#endif
     // render_kernel's ray tallies: one plain store per wave into this slot's
     // buffer, reduced after the launch on the same stream (an atomic per wave
     // holds the wave's slot for its round trip: C2 -13 %, C3 -4 %)

@@ -77,13 +77,14 @@ struct LptSlot {
     GrowBuf cost, cost_sorted, iota, order, scratch;
     GrowBuf wave_counts;  // render_kernel's per-wave ray tallies (rtd::FrameDev::wave_counts)
     GrowBuf hints;        // render_kernel's shadow-packet occluder hints (rtd::FrameDev::shadow_hint)
-    GrowBuf work, work_count;  // the sky pre-pass's tile list and its length (rtd::FrameDev::work)
+    unsigned long long hints_scene = ~0ull;  // the scene version and layout the hints were recorded for
+    long long hints_key = -1;
     long long key = -1;
     unsigned long long scene = ~0ull;
     bool valid = false;
     long long frames = 0;
     void release() {
-        for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch, &wave_counts, &hints, &work, &work_count}) {
+        for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch, &wave_counts, &hints}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;

@@ -223,7 +223,6 @@ __device__ __forceinline__ void store_pixel(const rtd::FrameDev &F, size_t idx, 
 // instructions instead of an integer-division sequence on the tile's critical
 // path.  Exact for every non-negative 32-bit tile.
 __device__ __forceinline__ void tile_xy(const rtd::FrameDev &F, int tile, int &tx, int &ty) {
-#ifdef RT_EXP_LEAN
     unsigned q = __umulhi((unsigned)tile, F.tiles_x_magic);
     int r = tile - (int)q * F.tiles_x;
     if (r >= F.tiles_x) {
@@ -232,10 +231,6 @@ __device__ __forceinline__ void tile_xy(const rtd::FrameDev &F, int tile, int &t
     }
     tx = r;
     ty = (int)q;
-#else
-    ty = tile / F.tiles_x;
-    tx = tile - ty * F.tiles_x;
-#endif
 }
 
 // The pixel rectangle of a tile (image rows; tile index wave-uniform) for the

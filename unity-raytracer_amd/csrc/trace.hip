@@ -211,7 +211,7 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 // shadow rays to each light: packet.h, scalar node fetches); the mirror
 // chain below it (a few percent of samples) runs per lane (shade_levels).
 // The counting launch keeps the per-ray traversal's canonical counts.
-template <bool COUNT, bool DEEP>
+template <bool COUNT, bool DEEP, bool HINT>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
                                          int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs, int tile) {
     (void)sg;
@@ -225,12 +225,10 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     RT_SEG(sg.visits += P.nodes + ((unsigned long long)P.leaves << 32);
            const unsigned long long tq1 = __builtin_amdgcn_s_memtime(); sg.setup = tq0; sg.prim = tq1 - tq0;)
     if (P.best_rank < 0) return rtt::ld3(F.bg255);  // :310-311
-#ifdef RT_EXP_LASTOCC
-    // this tile's occluder hints of the last frame (one per light, < kHintLights)
-    int *const hints = F.shadow_hint ? F.shadow_hint + (size_t)tile * kHintLights : nullptr;
+    // HINT: this tile's occluder hints of the last frame (one per light, < kHintLights)
+    int *const hints = HINT && F.shadow_hint ? F.shadow_hint + (size_t)tile * kHintLights : nullptr;
     int4 hv = make_int4(0, 0, 0, 0);
-    if (hints) hv = rtt::cload(reinterpret_cast<const int4 *>(hints));
-#endif
+    if (HINT && hints) hv = rtt::cload(reinterpret_cast<const int4 *>(hints));
     const rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
@@ -244,14 +242,10 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         rtt::setup_ray(rs, sr.o, sr.dir);
         rtp::PacketLane Q;
         RT_SEG(const unsigned long long tw0 = __builtin_amdgcn_s_memtime();)
-#ifdef RT_EXP_LASTOCC
-        const bool hl = hints && l < kHintLights;
+        const bool hl = HINT && hints && l < kHintLights;
         const int h = !hl ? 0 : l == 0 ? hv.x : l == 1 ? hv.y : l == 2 ? hv.z : hv.w;
-        rtp::packet_trace<true, COUNT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr, h,
-                                       hl ? hints + l : nullptr);
-#else
-        rtp::packet_trace<true, COUNT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
-#endif
+        rtp::packet_trace<true, COUNT, HINT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr, h,
+                                             hl ? hints + l : nullptr);
         RT_SEG(sg.shadow += __builtin_amdgcn_s_memtime() - tw0;
                sg.visits += Q.nodes + ((unsigned long long)Q.leaves << 32);)
         if (moot || Q.best_rank == 1) continue;
@@ -286,15 +280,13 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // one of the four (pshift 4: 16 lanes) or sixteen (pshift 2: 4 lanes) waves
 // an expensive tile is split into.
 // Returns true when the tile was answered by the sky test (no exact rays).
-template <bool COUNT, bool DEEP, bool Q4>
+template <bool COUNT, bool DEEP, bool Q4, bool HINT>
 __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
-                                            SegClock &sg, bool sky_done = false) {
-#ifdef RT_EXP_LEAN
+                                            SegClock &sg) {
     // the cut entries do not depend on the tile: their loads are issued first
     rtp::CutLane cl;
     if (!COUNT) cl = rtp::cut_load(S);
-#endif
     int px, ly, gy, s;
     const bool active =
         rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
@@ -303,16 +295,11 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     // without its exact rays (shade.h sky_maybe; the counting launch traces all)
     bool sky = false;
 #ifndef RT_EXP_NOSKY
-    // (sky_done: the sky pre-pass has answered this frame's sky tiles already)
-    if (!COUNT && !sky_done) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4>(F, px, gy, s))) == 0;
+    if (!COUNT) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4>(F, px, gy, s))) == 0;
 #endif
     // the camera packet's start below the top-level cut (every lane active here)
     rtp::CutStart cs = {0, 0, 0, -1};
-#ifdef RT_EXP_LEAN
     if (!COUNT && !sky && F.cut_test) cs = rtp::cut_select(S, F, rts::tile_rect<Q4>(F, tile), wstack, &cl);
-#else
-    if (!COUNT && !sky && F.cut_test) cs = rtp::cut_select(S, F, rts::tile_rect<Q4>(F, tile), wstack);
-#endif
     if (active) {
         if (COUNT) cnt.primary += 1;  // otherwise F.primary_total, added once per launch
         if (sky) {
@@ -326,7 +313,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
                 cnt.scene_miss +=
                     !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
             }
-            color = shade_path<COUNT, DEEP>(S, F, o, d, st, wstack, cnt, sg, cs, tile);
+            color = shade_path<COUNT, DEEP, HINT>(S, F, o, d, st, wstack, cnt, sg, cs, tile);
         }
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
@@ -338,9 +325,6 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     const int lane2 = rtt::lane_id();
     const bool active2 =
         rts::slot_pixel<Q4>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
-#ifdef RT_EXP_SKYNOSTORE
-    if (sky) return sky;  // measurement only: what a sky wave's pixel store costs
-#endif
     if (active2 && s == 0) {
         f3 v = sum;
         if (Q4)
@@ -392,19 +376,7 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     // the tile index is wave-uniform and kept in an SGPR: the slot -> pixel
     // integer math runs on the scalar unit and nothing of it is spilled
     int tile = idx;
-#ifdef RT_EXP_SKYPASS
-    // after the sky pre-pass: only the tiles it left, in dispatch order
-    const bool sky_done = !COUNT && !SPLIT && F.work;
-    if (sky_done) {
-        if (wid >= (int)rtt::cload(F.work_count)) return;  // wave-uniform
-        tile = rtt::cload(F.work + wid);
-    } else if (F.tile_order) {
-        tile = rtt::cload(F.tile_order + idx);
-    }
-#else
-    const bool sky_done = false;
     if (F.tile_order) tile = rtt::cload(F.tile_order + idx);
-#endif
     tile = __builtin_amdgcn_readfirstlane(tile);
     // the launch's camera samples (one per active lane of every tile, computed
     // by the host: rt_device.h active_samples), counted once per launch
@@ -412,7 +384,7 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    const bool sky = render_tile<COUNT, DEEP, Q4>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, sky_done);
+    const bool sky = render_tile<COUNT, DEEP, Q4, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
@@ -473,9 +445,7 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
 // launch never does).
 __global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n, unsigned tag,
                                                          unsigned long long primary_total,
-                                                         unsigned long long *counters, unsigned *work_count) {
-    // the sky pre-pass's counter, for the next frame (the launch that read it has ended)
-    if (work_count && blockIdx.x == 0 && threadIdx.x == 0) *work_count = 0u;
+                                                         unsigned long long *counters) {
     unsigned long long sh = 0, rf = 0, mo = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
         const uint4 v = wc[i];
@@ -507,55 +477,6 @@ __global__ __launch_bounds__(256) void wave_counts_kernel(const uint4 *wc, int n
         if (b) atomicAdd(ctr + 2, b);
         if (c) atomicAdd(ctr + 8, c);
     }
-}
-
-// Sky pre-pass (frames whose tiles render_kernel dispatches unsplit, sky test
-// on): one thread per tile in dispatch order runs the same per-sample test as
-// render_tile (shade.h sky_maybe, every slot of the tile) and answers a sky
-// tile at once — the background, summed and scaled exactly as render_tile
-// sums a sky wave's samples, stored for each of its pixels
-// (RayTracingSetup.cs:310-311) — and records a zero cost key; the other tiles
-// are appended to F.work (one atomic per wave, the wave's order kept), which
-// render_kernel then dispatches instead of the whole frame.  The heavy
-// megakernel waves (96 VGPRs, LDS stacks) are spent on tiles with rays only.
-template <bool Q4>
-__global__ __launch_bounds__(256) void sky_pass_kernel(SceneDev S, FrameDev F) {
-    (void)S;
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    bool keep = false;
-    int tile = 0;
-    if (idx < F.num_tiles) {
-        tile = F.tile_order ? F.tile_order[idx] : idx;
-        bool maybe = false;
-        for (int j = 0; j < kWaveSize && !maybe; ++j) {
-            int px, ly, gy, s;
-            if (rts::slot_pixel<Q4>(F, tile, j, px, ly, gy, s) && rts::sky_maybe<Q4>(F, px, gy, s)) maybe = true;
-        }
-        keep = maybe;
-        if (!maybe) {
-            const f3 c = rtt::ld3(F.bg255);
-            const int spp = Q4 ? 4 : F.spp;
-            f3 sum = c;  // sample_sum's order: ((s0 + s1) + s2) + ...
-            for (int k = 1; k < spp; ++k) sum = sum + c;
-            f3 v = sum;
-            if (Q4)
-                v = v * 0.25f;
-            else if (spp > 1)
-                v = (spp & (spp - 1)) == 0 ? v * F.inv_spp : v / (float)spp;
-            for (int j = 0; j < kWaveSize; j += spp) {
-                int px, ly, gy, s;
-                if (rts::slot_pixel<Q4>(F, tile, j, px, ly, gy, s)) rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
-            }
-            if (F.tile_cost) F.tile_cost[tile] = 0u;
-        }
-    }
-    const unsigned long long m = __ballot(keep);
-    if (m == 0) return;
-    unsigned base = 0;
-    const int lane = threadIdx.x & 63;
-    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(F.work_count, (unsigned)__popcll(m));
-    base = __shfl(base, __ffsll((long long)m) - 1);
-    if (keep) F.work[base + __popcll(m & ((1ull << lane) - 1))] = tile;
 }
 
 // The frame's sharded counters summed into kCounterWords words (out: the
@@ -837,11 +758,6 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     F.primary_total = active_samples(F.res_x, F.res_y, F.local_rows, F.row0, F.band_index, F.band_count, F.band_rows,
                                      F.spp);
     int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
-#ifdef RT_EXP_DROP_TAIL
-    // measurement only: the last RT_EXP_DROP_TAIL waves of the longest-first
-    // order (the sky tiles) are not launched (their pixels are left as they were)
-    blocks = blocks > RT_EXP_DROP_TAIL ? blocks - RT_EXP_DROP_TAIL : 0;
-#endif
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)
@@ -859,22 +775,17 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         if (e != hipSuccess || !F.wave_counts) return e;
         const int waves = F.num_tiles;  // one wave per tile, no splits
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
-                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters,
-                           F.work_count);
+                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
         return hipGetLastError();
     }
-    else if (q4) {
-        if (F.work) hipLaunchKernelGGL(sky_pass_kernel<true>, dim3((F.num_tiles + 255) / 256), dim3(256), 0, stream, S, F);
+    else if (q4)
         hipLaunchKernelGGL((render_kernel<false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    } else {
-        if (F.work) hipLaunchKernelGGL(sky_pass_kernel<false>, dim3((F.num_tiles + 255) / 256), dim3(256), 0, stream, S, F);
+    else
         hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    }
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
-                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters,
-                           F.work_count);
+                           (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
     }
     return hipGetLastError();
 }

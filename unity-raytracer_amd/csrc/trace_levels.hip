@@ -47,15 +47,24 @@ constexpr int kLvWavesHighSpp = 7;
 // and +15 % on C5 here (per-wave selection cost on 1- and 4-pixel tiles, more
 // spills in the level loop; round 3, tools/exp/ab_cfg.sh).
 
+// Lane state kept in LDS across a shadow packet (per instance): the 6-wave
+// (<= 16 spp) instance stashes the hit (point, normal, view), the colour with
+// and without the light and the mirror chain's term — 18 floats a lane, 4.5
+// KB a wave — instead of spilling them around the packet loop: C4 HBM writes
+// 4.40 -> 0.30 GB per launch, kernel -3 % single frame / -5 % frames in flight
+// (profiles/r04/).  The 7-wave (64 spp) instance keeps none: at 28 waves per
+// CU the LDS would cap it at 6 (C5 +6 %, and +3 % at 6 waves/SIMD).
+#ifdef RT_EXP_LVSTASH_HI
+constexpr int kLvStashHigh = RT_EXP_LVSTASH_HI;  // measuring builds only (0, 9 or 18)
+#else
+constexpr int kLvStashHigh = 0;
+#endif
 template <int MIN_WAVES>
 __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
-#ifdef RT_EXP_LVSTASH
-    // the lane state that lives across a shadow packet, kept in LDS instead of
-    // registers the packet's own values would spill (volatile: reloaded, so
-    // the register copies die at the store)
-    __shared__ float stash_mem[18 * kWaveSize];
-#endif
+    constexpr int STASH = MIN_WAVES == kLvWavesLowSpp ? 18 : kLvStashHigh;  // floats per lane
+    // (volatile: reloaded after the packet, so the register copies die at the store)
+    __shared__ float stash_mem[(STASH > 0 ? STASH : 1) * kWaveSize];
     const int lane = threadIdx.x & 63;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x;
@@ -117,25 +126,25 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
             rtt::RayCtx rs;
             rtt::setup_ray(rs, sr.o, sr.dir);
             rtp::PacketLane Q;
-#ifdef RT_EXP_LVSTASH
-            volatile float *vs = stash_mem + rtt::lane_id();
-            {
-                const float v[18] = {col.x, col.y, col.z, lit.x, lit.y, lit.z, sf.p.x, sf.p.y, sf.p.z,
-                                     sf.n.x, sf.n.y, sf.n.z, sf.view.x, sf.view.y, sf.view.z, term.x, term.y, term.z};
+            if (STASH > 0) {
+                volatile float *vs = stash_mem + rtt::lane_id();
+                const float v[18] = {col.x, col.y, col.z, lit.x, lit.y, lit.z, term.x, term.y, term.z,
+                                     sf.p.x, sf.p.y, sf.p.z, sf.n.x, sf.n.y, sf.n.z, sf.view.x, sf.view.y, sf.view.z};
 #pragma unroll
-                for (int i = 0; i < 18; ++i) vs[i * kWaveSize] = v[i];
+                for (int i = 0; i < STASH; ++i) vs[i * kWaveSize] = v[i];
+                rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+                vs = stash_mem + rtt::lane_id();
+                col = mk(vs[0], vs[64], vs[128]);
+                lit = mk(vs[192], vs[256], vs[320]);
+                term = mk(vs[384], vs[448], vs[512]);
+                if (STASH >= 18) {
+                    sf.p = mk(vs[576], vs[640], vs[704]);
+                    sf.n = mk(vs[768], vs[832], vs[896]);
+                    sf.view = mk(vs[960], vs[1024], vs[1088]);
+                }
+            } else {
+                rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
             }
-            rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
-            vs = stash_mem + rtt::lane_id();
-            col = mk(vs[0], vs[64], vs[128]);
-            lit = mk(vs[192], vs[256], vs[320]);
-            sf.p = mk(vs[384], vs[448], vs[512]);
-            sf.n = mk(vs[576], vs[640], vs[704]);
-            sf.view = mk(vs[768], vs[832], vs[896]);
-            term = mk(vs[960], vs[1024], vs[1088]);
-#else
-            rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
-#endif
             if (trace && Q.best_rank != 1) col = lit;
         }
         bool mirror = false;
