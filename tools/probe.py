@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--no-lights", action="store_true")
     ap.add_argument("--band", default="", help="i/n: render only row band i of n (8-row blocks): a light load")
     ap.add_argument("--rgb32f", action="store_true", help="float RGB output (the bench's shard format at N > 1)")
+    ap.add_argument("--async-frames", action="store_true",
+                    help="timed frames with RT_FLAG_ASYNC, as bench.py times them (the same kernel instance: "
+                         "synchronous whole frames split their slowest tiles, asynchronous ones do not)")
     a = ap.parse_args()
     rt = _rt_pkg.load()
     fr = rt.make(a.config)
@@ -76,7 +79,16 @@ def main():
             for _ in range(2):
                 ctx.render_device(fr.camera, fr.plane, p, out.data_ptr(), out.numel() * 4)
             ks, ts = [], []
-            for _ in range(a.frames):
+            if a.async_frames:
+                pa = rt.frame_params(fr, flags=flags | rt.abi.RT_FLAG_ASYNC, **bkw)
+                for _ in range(a.frames):
+                    ctx.render_device(fr.camera, fr.plane, pa, out.data_ptr(), out.numel() * 4)
+                st = ctx.finish()
+                for f_ in ("primary_rays", "shadow_rays", "reflection_rays"):
+                    setattr(st, f_, getattr(st, f_) // a.frames)
+                ks.append(st.kernel_ms / a.frames)
+                ts.append(st.total_ms / a.frames)
+            for _ in range(0 if a.async_frames else a.frames):
                 st = ctx.render_device(fr.camera, fr.plane, p, out.data_ptr(), out.numel() * 4)
                 ks.append(st.kernel_ms)
                 ts.append(st.total_ms)

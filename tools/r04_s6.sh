@@ -11,12 +11,12 @@ tag=${1:-r04g}
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   > gpurun_out/tests_$tag.log 2>&1 || { echo tests-fail; tail -40 gpurun_out/tests_$tag.log; exit 1; }
 tail -1 gpurun_out/tests_$tag.log
-timeout -k 10 300 python tools/abx.py --config C3 --variants base,default --rounds 10 --frames 12 \
+timeout -k 10 300 python tools/abx.py --config C3 --variants base,default,st8w6,leaf4 --rounds 10 --frames 12 \
   > gpurun_out/abx_$tag.log 2>&1 || { echo abx-fail; tail gpurun_out/abx_$tag.log; exit 1; }
 timeout -k 10 300 python tools/abx.py --config C3 --band 0/8 --variants base,default --rounds 10 --frames 12 \
   >> gpurun_out/abx_$tag.log 2>&1 || { echo abx-b8-fail; exit 1; }
 for c in C4 C5 C2; do
-  timeout -k 10 300 python tools/abx.py --config $c --variants base,default,lvhi9 --rounds 6 --frames 6 \
+  timeout -k 10 300 python tools/abx.py --config $c --variants base,default,lvhi9,xcd,leaf4 --rounds 6 --frames 6 \
     >> gpurun_out/abx_$tag.log 2>&1 || { echo abx-$c-fail; exit 1; }
 done
 grep variant gpurun_out/abx_$tag.log

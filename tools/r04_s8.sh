@@ -1,0 +1,42 @@
+# Round-4 GPU session 8: the final candidate build — GPU suite, smoke, A/B
+# against the round's base and the previous default, the bench line, the
+# single-stream kernel trace, the counter passes and the one-rank shares.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+tag=${1:-r04i}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+  > gpurun_out/tests_$tag.log 2>&1 || { echo tests-fail; tail -40 gpurun_out/tests_$tag.log; exit 1; }
+tail -1 gpurun_out/tests_$tag.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$tag.log 2>&1 || { echo smoke-fail; tail gpurun_out/smoke_$tag.log; exit 1; }
+tail -1 gpurun_out/smoke_$tag.log
+for c in C3 C2; do
+  timeout -k 10 300 python tools/abx.py --config $c --variants base,prev,default --rounds 8 --frames 12 \
+    >> gpurun_out/abx_$tag.log 2>&1 || { echo abx-$c-fail; tail gpurun_out/abx_$tag.log; exit 1; }
+done
+for b in 0/8 0/2; do
+  timeout -k 10 300 python tools/abx.py --config C3 --band $b --variants base,prev,default --rounds 8 --frames 12 \
+    >> gpurun_out/abx_$tag.log 2>&1 || { echo abx-b-fail; exit 1; }
+done
+grep variant gpurun_out/abx_$tag.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$tag.log 2>&1 || { echo bench-fail; tail -20 gpurun_out/bench_$tag.log; exit 1; }
+echo bench-ok
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/kt_$tag -o run --output-format csv -- \
+  python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --streams 1 --moving-frames 0 > $R/gpurun_out/kt_$tag.log 2>&1 || { echo kt-fail; exit 1; }
+echo kt-ok
+cd $R
+for cb in C3:1 C3:8 C4:1 C5:1; do
+  bash tools/pmc_round.sh $tag ${cb%%:*} ${cb##*:} > gpurun_out/pmcr_${tag}_${cb%%:*}_${cb##*:}.log 2>&1 || { echo pmc-fail-$cb; tail gpurun_out/pmcr_${tag}_${cb%%:*}_${cb##*:}.log; exit 1; }
+  echo pmc-ok-$cb
+done
+for n in 2 4 8; do
+  timeout -k 10 300 python bench.py --steps 100 --warmup 5 --no-cpu-baseline --sim-bands $n > gpurun_out/sb${n}_$tag.log 2>&1 || { echo sb$n-fail; exit 1; }
+  timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --sim-bands $n --streams 1 > gpurun_out/sb${n}s1_$tag.log 2>&1 || { echo sb${n}s1-fail; exit 1; }
+done
+for c in C4 C5; do
+  timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --moving-frames 0 > gpurun_out/bench_${c}_$tag.log 2>&1 || { echo bench-$c-fail; exit 1; }
+done
+echo ALLDONE

@@ -25,7 +25,16 @@
 
 namespace rtd {
 
-constexpr int kStackSize = 24;  // LDS traversal stack entries per lane
+// LDS traversal stack entries per lane (deeper entries: the private
+// overflow).  16 keeps a one-wave workgroup of the megakernel at 4.8 KB of
+// LDS, so six waves per SIMD fit a CU (trace.hip kMkMinWaves); 24 capped it
+// at 23 waves per CU.  Only per-lane traversals use it (mirror chains, the
+// counting launch, rt_intersect_rays).
+#ifdef RT_EXP_STACK
+constexpr int kStackSize = RT_EXP_STACK;  // measuring builds only
+#else
+constexpr int kStackSize = 16;
+#endif
 constexpr int kStackTotal = 128;         // + private (scratch) overflow: >= 3 * BVH4 depth, >= LBVH depth
 constexpr int kMaxTreeDepth = 31;         // builder guarantees BVH2 internal depth <= 31
 constexpr int kMaxBounces = 32;     // per-lane mirror fold stack

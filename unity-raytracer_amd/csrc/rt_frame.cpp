@@ -239,6 +239,11 @@ constexpr int kSplit16MaxTiles = RT_EXP_SPLIT16MAX;  // measuring builds only
 constexpr int kSplit16MaxTiles = 70000;
 #endif
 constexpr int kSplit16DivLarge = 4096;
+#ifdef RT_EXP_NOSYNCSPLIT
+constexpr bool kSplitSync = false;  // measuring builds only
+#else
+constexpr bool kSplitSync = true;
+#endif
 // A synchronous frame (no RT_FLAG_ASYNC: Update() waits for it, RayTracingSetup.cs:
 // 171-199) has no next frame to hide its tail behind, so whole frames of any size
 // split their slowest 1/4096 into sixteenth-waves too: C3 single frame -9 % (0.290 ->
@@ -397,7 +402,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
             F.split_tiles -= F.split16_tiles;
         }
     } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
-               (F.num_tiles <= kSplit16MaxTiles || (prm->flags & RT_FLAG_ASYNC) == 0)) {
+               (F.num_tiles <= kSplit16MaxTiles || (kSplitSync && (prm->flags & RT_FLAG_ASYNC) == 0))) {
         F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
     }
     // the split-tile instance's shadow occluder hints (packet.h packet_trace
@@ -414,6 +419,13 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         ls->hints_scene = ctx->scene_version;
         ls->hints_key = key;
         F.shadow_hint = (int *)ls->hints.p;
+    }
+    if (levels && !(F.max_bounces > rtd::kMaxBounces)) {
+        // the levels kernel dispatches XCD-aware stripes in row order
+        // (trace_levels.hip): no longest-first order, no cost measurement
+        F.tile_order = nullptr;
+        F.tile_cost = nullptr;
+        lpt_sort = false;
     }
     // render_kernel's ray tallies: one plain store per wave into this slot's
     // buffer, reduced after the launch on the same stream (an atomic per wave

@@ -213,7 +213,9 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 // The counting launch keeps the per-ray traversal's canonical counts.
 template <bool COUNT, bool DEEP, bool HINT>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
-                                         int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs, int tile) {
+                                         int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs, int tile,
+                                         float *stash) {
+    (void)stash;
     (void)sg;
     (void)tile;
     if (COUNT || !S.bvh4) return shade_levels<COUNT, DEEP>(S, F, o, d, 0, st, cnt);
@@ -229,7 +231,11 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     int *const hints = HINT && F.shadow_hint ? F.shadow_hint + (size_t)tile * kHintLights : nullptr;
     int4 hv = make_int4(0, 0, 0, 0);
     if (HINT && hints) hv = rtt::cload(reinterpret_cast<const int4 *>(hints));
+#ifdef RT_EXP_MKSTASH
+    rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
+#else
     const rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
+#endif
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
         const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
@@ -244,13 +250,43 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         RT_SEG(const unsigned long long tw0 = __builtin_amdgcn_s_memtime();)
         const bool hl = HINT && hints && l < kHintLights;
         const int h = !hl ? 0 : l == 0 ? hv.x : l == 1 ? hv.y : l == 2 ? hv.z : hv.w;
+#ifdef RT_EXP_MKSTASH
+        // the hit's state lives in LDS across the shadow packet (volatile:
+        // reloaded after it, so its registers die at the store)
+        rts::Surface sfl = sf;
+        f3 litl = lit, coll = col;
+        {
+            volatile float *vs = stash + rtt::lane_id();
+            const float v[15] = {coll.x, coll.y, coll.z, litl.x, litl.y, litl.z, sfl.p.x, sfl.p.y, sfl.p.z,
+                                 sfl.n.x, sfl.n.y, sfl.n.z, sfl.view.x, sfl.view.y, sfl.view.z};
+#pragma unroll
+            for (int i = 0; i < 15; ++i) vs[i * kWaveSize] = v[i];
+        }
+#endif
         rtp::packet_trace<true, COUNT, HINT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr, h,
                                              hl ? hints + l : nullptr);
+#ifdef RT_EXP_MKSTASH
+        {
+            volatile float *vs = stash + rtt::lane_id();
+            coll = mk(vs[0], vs[64], vs[128]);
+            litl = mk(vs[192], vs[256], vs[320]);
+            sfl.p = mk(vs[384], vs[448], vs[512]);
+            sfl.n = mk(vs[576], vs[640], vs[704]);
+            sfl.view = mk(vs[768], vs[832], vs[896]);
+        }
+        sf = sfl;
+        col = coll;
+        const f3 lit2 = litl;
+#define RT_LIT lit2
+#else
+#define RT_LIT lit
+#endif
         RT_SEG(sg.shadow += __builtin_amdgcn_s_memtime() - tw0;
                sg.visits += Q.nodes + ((unsigned long long)Q.leaves << 32);)
         if (moot || Q.best_rank == 1) continue;
-        col = lit;
+        col = RT_LIT;
     }
+#undef RT_LIT
     const DevMaterial m = S.mats[sf.mat];
     if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363
         cnt.reflection++;
@@ -262,11 +298,20 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     return col;
 }
 
+// Waves per SIMD the register budget must allow.  Whole frames: 6 (80
+// VGPRs) — with the per-lane LDS stack at 16 entries (rt_device.h
+// kStackSize) six waves fit a CU's LDS too; at 24 entries the LDS capped the
+// CU at 23 one-wave workgroups, so earlier "6 waves" builds only spilled more.
+// C3 -7 % single frame / -5 % frames in flight, C2 -5 % / -2 % (r04h).  Small
+// frames (row shards of <= kShardTiles tiles, whose time is their slowest
+// waves): 5 (96 VGPRs, fewer spills) — 6 made a 1/8 shard 3-9 % slower.
 #ifdef RT_EXP_MKWAVES
 constexpr int kMkMinWaves = RT_EXP_MKWAVES;  // measuring builds only
 #else
-constexpr int kMkMinWaves = 5;  // waves per SIMD the register budget must allow (96 VGPRs)
+constexpr int kMkMinWaves = 6;
 #endif
+constexpr int kMkMinWavesShard = 5;
+constexpr int kShardTiles = 70000;  // rt_frame.cpp kSplit16MaxTiles: a 1/2 shard of 1080p at 4 spp
 // Waves per megakernel workgroup.  A workgroup's slot is recycled only when
 // all of its waves are done, and path lengths vary a lot between tiles, so
 // small workgroups keep the CUs fuller near the end of each wave "round".
@@ -283,7 +328,7 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 template <bool COUNT, bool DEEP, bool Q4, bool HINT>
 __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
-                                            SegClock &sg) {
+                                            SegClock &sg, float *stash) {
     // the cut entries do not depend on the tile: their loads are issued first
     rtp::CutLane cl;
     if (!COUNT) cl = rtp::cut_load(S);
@@ -313,7 +358,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
                 cnt.scene_miss +=
                     !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
             }
-            color = shade_path<COUNT, DEEP, HINT>(S, F, o, d, st, wstack, cnt, sg, cs, tile);
+            color = shade_path<COUNT, DEEP, HINT>(S, F, o, d, st, wstack, cnt, sg, cs, tile, stash);
         }
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
@@ -341,10 +386,16 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
 // the common kernel's code and register allocation stay as they are); DEEP:
 // the one for MaxReflectionBounces > kMaxBounces (deep_chain); Q4: frames of
 // 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel).
-template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false>
-__global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDev S, FrameDev F) {
+template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false, int W = kMkMinWaves>
+__global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
     __shared__ int wstack_mem[kMkWaves * rtp::kWaveStack];
+#ifdef RT_EXP_MKSTASH
+    __shared__ float stash_mem[kMkWaves * 15 * kWaveSize];
+    float *const stash = stash_mem;  // (one wave per workgroup)
+#else
+    float *const stash = nullptr;
+#endif
     const int lane = threadIdx.x & 63;
     // wave-uniform (an SGPR; with one-wave workgroups simply the block index)
     const int wave = kMkWaves == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -384,7 +435,7 @@ __global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_kernel(SceneDe
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    const bool sky = render_tile<COUNT, DEEP, Q4, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    const bool sky = render_tile<COUNT, DEEP, Q4, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, stash);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
@@ -759,15 +810,26 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
                                      F.spp);
     int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
+    const bool shard = F.num_tiles <= kShardTiles;  // a small frame: its slowest waves set its time
+    constexpr int W5 = kMkMinWavesShard;
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)
-            hipLaunchKernelGGL((render_kernel<true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+            hipLaunchKernelGGL((render_kernel<true, false, true, false, W5>), dim3(blocks), dim3(kMkThreads), 0, stream,
+                               S, F);
         else
-            hipLaunchKernelGGL((render_kernel<false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+            hipLaunchKernelGGL((render_kernel<false, false, true, false, W5>), dim3(blocks), dim3(kMkThreads), 0,
+                               stream, S, F);
     } else if (count_tests)
-        hipLaunchKernelGGL(render_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+        hipLaunchKernelGGL((render_kernel<true, false, false, false, W5>), dim3(blocks), dim3(kMkThreads), 0, stream, S,
+                           F);
+    else if ((F.split_tiles > 0 || F.split16_tiles > 0) && q4 && shard)
+        hipLaunchKernelGGL((render_kernel<false, true, false, true, W5>), dim3(blocks), dim3(kMkThreads), 0, stream, S,
+                           F);
     else if ((F.split_tiles > 0 || F.split16_tiles > 0) && q4)
         hipLaunchKernelGGL((render_kernel<false, true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+    else if ((F.split_tiles > 0 || F.split16_tiles > 0) && shard)
+        hipLaunchKernelGGL((render_kernel<false, true, false, false, W5>), dim3(blocks), dim3(kMkThreads), 0, stream, S,
+                           F);
     else if (F.split_tiles > 0 || F.split16_tiles > 0)
         hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
     else if (S.bvh4 && F.spp >= kLevelsMinSpp) {

@@ -54,6 +54,8 @@ constexpr int kLvWavesHighSpp = 7;
 // 4.40 -> 0.30 GB per launch, kernel -3 % single frame / -5 % frames in flight
 // (profiles/r04/).  The 7-wave (64 spp) instance keeps none: at 28 waves per
 // CU the LDS would cap it at 6 (C5 +6 %, and +3 % at 6 waves/SIMD).
+constexpr int kXcdStripeRows = 4;  // tile rows per XCD stripe (render_levels_kernel dispatch)
+
 #ifdef RT_EXP_LVSTASH_HI
 constexpr int kLvStashHigh = RT_EXP_LVSTASH_HI;  // measuring builds only (0, 9 or 18)
 #else
@@ -67,12 +69,18 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     __shared__ float stash_mem[(STASH > 0 ? STASH : 1) * kWaveSize];
     const int lane = threadIdx.x & 63;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
-    const int wid = blockIdx.x;
-    if (wid >= F.num_tiles) return;  // wave-uniform
+    // XCD-aware dispatch (blocks b and b + 8 share an XCD, MI355X_MICROARCH.md
+    // "Workgroup dispatch"; placement is a speed matter only): XCD group x
+    // renders the stripes x, x + 8, ... of kXcdStripeRows tile rows in row
+    // order, so each XCD's L2 serves the geometry of one eighth of the screen
+    // instead of all of it — C5 -3 %, C4 -2 % with frames in flight (r04g).
+    // A frame's tiles are all here exactly once, whatever the placement.
+    const int zs = kXcdStripeRows * F.tiles_x;
+    const int k = blockIdx.x >> 3;
+    const int wid = ((k / zs) * 8 + (blockIdx.x & 7)) * zs + k % zs;  // the tile itself
+    if (wid >= F.num_tiles) return;  // wave-uniform (the last stripes' padding)
     // the tile index in an SGPR (scalar slot -> pixel math, nothing spilled)
-    int tile = wid;
-    if (F.tile_order) tile = rtt::cload(F.tile_order + wid);
-    tile = __builtin_amdgcn_readfirstlane(tile);
+    int tile = __builtin_amdgcn_readfirstlane(wid);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
@@ -202,11 +210,14 @@ namespace rtk {
 
 hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
+    // whole groups of eight stripes (render_levels_kernel's XCD-aware dispatch)
+    const long long zs = (long long)kXcdStripeRows * F.tiles_x, ns = (F.num_tiles + zs - 1) / zs;
+    const long long grid = 8 * ((ns + 7) / 8) * zs;
+    if (grid > 0x7fffffffll) return hipErrorInvalidValue;
     if (F.spp <= 16)
-        hipLaunchKernelGGL(render_levels_kernel<kLvWavesLowSpp>, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S, F);
+        hipLaunchKernelGGL(render_levels_kernel<kLvWavesLowSpp>, dim3((unsigned)grid), dim3(kWaveSize), 0, stream, S, F);
     else
-        hipLaunchKernelGGL(render_levels_kernel<kLvWavesHighSpp>, dim3(F.num_tiles), dim3(kWaveSize), 0, stream, S,
-                           F);
+        hipLaunchKernelGGL(render_levels_kernel<kLvWavesHighSpp>, dim3((unsigned)grid), dim3(kWaveSize), 0, stream, S, F);
     return hipGetLastError();
 }
 
