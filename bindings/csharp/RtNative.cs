@@ -193,6 +193,7 @@ namespace RayTracer.Native
                                                                    [Out] RtHit[] hits);
         [DllImport(Lib)] public static extern float rt_spec_threshold();
         [DllImport(Lib)] public static extern int rt_debug_set(IntPtr ctx, int what, int value);  // tests only
+        [DllImport(Lib)] public static extern int rt_debug_read(IntPtr ctx, int what, IntPtr output, long capacityBytes, out long bytesWritten);  // measuring builds only
 
         public static string LastError(IntPtr ctx) => Marshal.PtrToStringAnsi(rt_last_error(ctx));
 

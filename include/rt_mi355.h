@@ -417,7 +417,18 @@ float rt_spec_threshold(void);
  * slab `value` (-1: off), so the error path's cleanup — every copy posted
  * for the earlier slabs finished before rt_render returns — can be tested. */
 #define RT_DEBUG_FAIL_SLAB 1
+/* Measuring only: RT_DEBUG_WAVE_CLOCKS (value 1: on, 0: off) makes every
+ * render_kernel launch record, per wave, its start and duration on the GPU's
+ * constant 100 MHz clock; rt_debug_read(ctx, RT_DEBUG_WAVE_CLOCKS, ...) returns
+ * the last launch's records (waits for the device).  A record is 4 uint32:
+ * start (low, high word), duration, tile | (part + 1) << 24 (part: -1 whole
+ * tile, else the split tile's quarter / sixteenth); a zero record is a wave
+ * slot that did no tile.  The product build does not record (RT_E_STATE); a
+ * measuring build is compiled with -DRT_WAVE_CLOCK.  One
+ * frame in flight at a time: every launch overwrites the records. */
+#define RT_DEBUG_WAVE_CLOCKS 2
 int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value);
+int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, int64_t *bytes_written);
 
 #ifdef __cplusplus
 }

@@ -24,6 +24,17 @@ def seg_per_wave(st):
             "total_cyc": round(st.shading_fetches / w), "setup_cyc": round(st.primary_scene_misses / w)}
 
 
+def seg_levels_per_wave(st, waves):
+    """RT_SEG_PROFILE words of render_levels_kernel -> per-wave averages."""
+    w = max(1, waves)
+    vc, vs = st.box_tests, st.primary_scene_misses
+    cam, sh, tot = st.triangle_tests, st.sphere_tests, st.shading_fetches
+    return {"waves": w, "cam_nodes": round((vc & 0xffffffff) / w, 2), "cam_leaves": round((vc >> 32) / w, 2),
+            "shadow_nodes": round((vs & 0xffffffff) / w, 2), "shadow_leaves": round((vs >> 32) / w, 2),
+            "cam_cyc": round(cam / w), "shadow_cyc": round(sh / w), "total_cyc": round(tot / w),
+            "rest_cyc": round((tot - cam - sh) / w)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
@@ -104,7 +115,11 @@ def main():
                               # first shadow packet, whole tile) in the test-counter words of a timed frame
                               **({"seg_cycles": [st.box_tests, st.triangle_tests, st.sphere_tests,
                                                  st.shading_fetches],
-                                  "seg_per_wave": seg_per_wave(st)} if "seg" in v else {})}), flush=True)
+                                  "seg_per_wave": seg_per_wave(st)} if "seg" in v and "seglv" not in v else {}),
+                              # render_levels_kernel (>= 16 spp): one wave per 64 samples
+                              **({"seg_levels_per_wave": seg_levels_per_wave(
+                                  st, fr.plane.ResolutionX * fr.plane.ResolutionY * fr.spp // 64)}
+                                 if "seglv" in v else {})}), flush=True)
         ctx.close()
 
 

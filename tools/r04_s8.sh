@@ -7,6 +7,8 @@ cd $R
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 tag=${1:-r04i}
+stage=${2:-a}
+if [ "$stage" = a ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   > gpurun_out/tests_$tag.log 2>&1 || { echo tests-fail; tail -40 gpurun_out/tests_$tag.log; exit 1; }
 tail -1 gpurun_out/tests_$tag.log
@@ -28,6 +30,16 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/kt_$tag -o r
   python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --streams 1 --moving-frames 0 > $R/gpurun_out/kt_$tag.log 2>&1 || { echo kt-fail; exit 1; }
 echo kt-ok
 cd $R
+timeout -k 10 300 python tools/wave_clock.py --config C3 --bands 1,2,4,8 > gpurun_out/wclk_$tag.log 2>&1 || { echo wclk-fail; tail gpurun_out/wclk_$tag.log; exit 1; }
+timeout -k 10 300 python tools/wave_clock.py --config C3 --bands 1,2,4,8 --async-frames >> gpurun_out/wclk_$tag.log 2>&1 || { echo wclk-async-fail; exit 1; }
+echo wclk-ok
+for c in C4 C5; do
+  timeout -k 10 300 python tools/probe.py --config $c --modes megakernel --frames 3 --variants seglv,default \
+    >> gpurun_out/seglv_$tag.log 2>&1 || { echo seglv-$c-fail; tail gpurun_out/seglv_$tag.log; exit 1; }
+done
+echo seglv-ok
+fi
+if [ "$stage" = b ]; then
 for cb in C3:1 C3:8 C4:1 C5:1; do
   bash tools/pmc_round.sh $tag ${cb%%:*} ${cb##*:} > gpurun_out/pmcr_${tag}_${cb%%:*}_${cb##*:}.log 2>&1 || { echo pmc-fail-$cb; tail gpurun_out/pmcr_${tag}_${cb%%:*}_${cb##*:}.log; exit 1; }
   echo pmc-ok-$cb
@@ -39,4 +51,5 @@ done
 for c in C4 C5; do
   timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --moving-frames 0 > gpurun_out/bench_${c}_$tag.log 2>&1 || { echo bench-$c-fail; exit 1; }
 done
+fi
 echo ALLDONE

@@ -33,6 +33,7 @@ RT_FLAG_ASYNC = 32
 RT_FLAG_ROW_ORDER = 64
 RT_FLAG_NO_CUT = 256
 RT_DEBUG_FAIL_SLAB = 1
+RT_DEBUG_WAVE_CLOCKS = 2
 RT_BUILD_SAH_HOST = 0
 RT_BUILD_LBVH_GPU = 1
 RT_BUILD_LBVH_GPU_BVH2 = 2
@@ -228,6 +229,7 @@ SIGNATURES = {
     "rt_assemble_bands_ex": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_intersect_rays": (C.c_int, [_P, _P, C.c_int32, _P]),
     "rt_debug_set": (C.c_int, [_P, C.c_int32, C.c_int32]),
+    "rt_debug_read": (C.c_int, [_P, C.c_int32, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]),
 }
 
 _lib = None
@@ -253,6 +255,8 @@ def load_library(path: str | None = None):
             "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
     lib = C.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
+        if path is not None and name.startswith("rt_debug") and not hasattr(lib, name):
+            continue  # an older measuring build (tools/abx.py variants) without a later testing entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -8,6 +8,15 @@
 
 namespace rtk {
 
+// Measuring builds (-DRT_WAVE_CLOCK): render_kernel records per-wave clocks
+// into F.wave_clock (rt_debug_set RT_DEBUG_WAVE_CLOCKS); the product build
+// compiles no such store.
+#ifdef RT_WAVE_CLOCK
+constexpr bool kWaveClockBuild = true;
+#else
+constexpr bool kWaveClockBuild = false;
+#endif
+
 // One frame (or one row shard of it): CastPixelRays + Shade, RayTracingSetup.cs:275-366.
 // Megakernel: one lane per sample, whole Whitted chain in one launch (trace.hip).
 // Longest-first tile order for the next frame (trace.hip).

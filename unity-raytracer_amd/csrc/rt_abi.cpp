@@ -338,7 +338,28 @@ int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value) {
         ctx->debug_fail_slab = value;
         return RT_OK;
     }
+    if (what == RT_DEBUG_WAVE_CLOCKS) {
+        if (!rtk::kWaveClockBuild)
+            return fail(ctx, RT_E_STATE, "RT_DEBUG_WAVE_CLOCKS: measuring builds only (-DRT_WAVE_CLOCK)");
+        ctx->debug_wave_clock = value != 0;
+        return RT_OK;
+    }
     return fail(ctx, RT_E_INVALID, "unknown rt_debug_set item %d", what);
+}
+
+int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, int64_t *bytes_written) {
+    if (!ctx) return RT_E_INVALID;
+    if (bytes_written) *bytes_written = 0;
+    if (what != RT_DEBUG_WAVE_CLOCKS) return fail(ctx, RT_E_INVALID, "unknown rt_debug_read item %d", what);
+    if (!ctx->debug_wave_clock) return fail(ctx, RT_E_STATE, "RT_DEBUG_WAVE_CLOCKS is off");
+    if (!out || capacity_bytes < 0) return fail(ctx, RT_E_INVALID, "rt_debug_read: null output or negative size");
+    DeviceGuard guard;
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    HIP_OR_FAIL(ctx, hipDeviceSynchronize());
+    const int64_t n = std::min<int64_t>(capacity_bytes, ctx->wave_clock_bytes);
+    if (n > 0) HIP_OR_FAIL(ctx, hipMemcpy(out, ctx->wave_clock.p, (size_t)n, hipMemcpyDeviceToHost));
+    if (bytes_written) *bytes_written = n;
+    return RT_OK;
 }
 
 }  // extern "C"

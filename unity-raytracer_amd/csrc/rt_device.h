@@ -258,6 +258,7 @@ struct FrameDev {
     int cut_test;
     float cut_ax[3], cut_bx[3], cut_ay[3], cut_by[3];
     float cut_a[3], cut_r[3], cut_u[3];  // A, R, U (the central ray's direction orders the entries)
+    uint4 *wave_clock;  // measuring builds only (RT_WAVE_CLOCK): per-wave {start lo, start hi, duration, tile}
 };
 
 }  // namespace rtd

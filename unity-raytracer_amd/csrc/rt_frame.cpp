@@ -440,6 +440,14 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         if (++ctx->count_tag == 0) ++ctx->count_tag;
         F.count_tag = ctx->count_tag;
     }
+    // measuring builds (rt_debug_set RT_DEBUG_WAVE_CLOCKS): the launch's per-wave clocks
+    if (rtk::kWaveClockBuild && ctx->debug_wave_clock && !count && !levels) {
+        const size_t bytes = (size_t)rtk::render_mega_waves(F) * sizeof(uint4);
+        HIP_OR_FAIL(ctx, ensure(ctx, ctx->wave_clock, bytes));
+        HIP_OR_FAIL(ctx, hipMemsetAsync(ctx->wave_clock.p, 0, bytes, ctx->stream));
+        F.wave_clock = (uint4 *)ctx->wave_clock.p;
+        ctx->wave_clock_bytes = (int64_t)bytes;
+    }
     return RT_OK;
 }
 

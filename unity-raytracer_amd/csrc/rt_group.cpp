@@ -81,6 +81,7 @@ void destroy_one(rt_ctx *ctx) {
     if (ctx->d_out) (void)hipFree(ctx->d_out);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_cut) (void)hipFree(ctx->d_cut);
+    if (ctx->wave_clock.p) (void)hipFree(ctx->wave_clock.p);
     if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
     if (ctx->h_update) (void)hipHostFree(ctx->h_update);
     if (ctx->ev_x) (void)hipEventDestroy(ctx->ev_x);

@@ -333,6 +333,10 @@ struct rt_ctx {
     bool warmed = false;  // the render kernels have run once on this device (warm_up)
     unsigned count_tag = 0;  // the last render_kernel launch's wave_counts tag
     int debug_fail_slab = -1;  // rt_debug_set(RT_DEBUG_FAIL_SLAB): rt_render fails before this row slab
+    // rt_debug_set(RT_DEBUG_WAVE_CLOCKS), measuring builds: the last render_kernel launch's per-wave clocks
+    bool debug_wave_clock = false;
+    rti::GrowBuf wave_clock;
+    int64_t wave_clock_bytes = 0;
 };
 
 namespace rti {

@@ -407,6 +407,9 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     const int split16 = SPLIT ? F.split16_tiles : 0;
     const int split = SPLIT ? F.split_tiles : 0;
     if (wid >= F.num_tiles + 15 * split16 + 3 * split) return;  // wave-uniform
+#ifdef RT_WAVE_CLOCK
+    const unsigned long long rc0 = __builtin_amdgcn_s_memrealtime();  // constant 100 MHz clock
+#endif
     // dispatch order: the previous frame's most expensive tiles first
     // (F.tile_order); SPLIT: the first split16_tiles of them as sixteen
     // waves of one pixel's 4 samples each, the next split_tiles as four
@@ -453,22 +456,21 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
             vi = max(vi, (unsigned long long)__shfl_xor((long long)vi, off));
         }
         if (lane == 0) {
-#ifdef RT_SEG_MAX
-            // the slowest wave instead of sums (slot 0 only: the host sums slots)
-            unsigned long long *ctr = F.counters;
-            atomicMax(ctr + 3, (vi & 0xffffffffull) + (vi >> 32));  // packet node + leaf visits
-            atomicMax(ctr + 4, pr);
-            atomicMax(ctr + 5, sh);
-            atomicMax(ctr + 6, ts1 - ts0);
-#else
             unsigned long long *ctr = F.counters + (size_t)(blockIdx.x % kCounterSlots) * kCounterWords;
             atomicAdd(ctr + 3, vi);  // packet visits: internal | leaves << 32
             atomicAdd(ctr + 4, pr);
             atomicAdd(ctr + 5, sh);
             atomicAdd(ctr + 6, ts1 - ts0);
             atomicAdd(ctr + 7, su);  // tile start -> camera packet (slot mapping, sky test, cut, primary ray)
-#endif
         }
+    }
+#endif
+#ifdef RT_WAVE_CLOCK
+    if (F.wave_clock && lane_e == 0) {
+        // plain vector store (the wave's start and duration; the host finds the slowest waves)
+        const unsigned long long rc1 = __builtin_amdgcn_s_memrealtime();
+        F.wave_clock[wid] = make_uint4((unsigned)rc0, (unsigned)(rc0 >> 32), (unsigned)(rc1 - rc0),
+                                       (unsigned)tile | ((unsigned)(part + 1) << 24));
     }
 #endif
 #ifndef RT_EXP_NOFLUSH

@@ -61,6 +61,17 @@ constexpr int kLvStashHigh = RT_EXP_LVSTASH_HI;  // measuring builds only (0, 9 
 #else
 constexpr int kLvStashHigh = 0;
 #endif
+// RT_SEG_PROFILE (profiling builds only): per-wave shader-clock time of the
+// camera packets (level 0), the shadow packets (every level), the mirror-ray
+// packets (levels >= 1) and the whole tile, plus the wave-level node / leaf
+// visits of the camera and shadow packets, summed into the (otherwise unused,
+// non-counting) test-counter words 3-7 (tools/probe.py reads them).
+#ifdef RT_SEG_PROFILE
+#define RT_LSEG(...) __VA_ARGS__
+#else
+#define RT_LSEG(...)
+#endif
+
 template <int MIN_WAVES>
 __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
@@ -82,6 +93,8 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     // the tile index in an SGPR (scalar slot -> pixel math, nothing spilled)
     int tile = __builtin_amdgcn_readfirstlane(wid);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
+    RT_LSEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
+            unsigned long long sg_cam = 0, sg_sh = 0, sg_mir = 0, sg_vcam = 0, sg_vsh = 0;)
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
     int depth = 0;
@@ -109,7 +122,15 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         rtt::RayCtx r;
         rtt::setup_ray(r, o, d);
         rtp::PacketLane P;
+        RT_LSEG(const unsigned long long tp0 = __builtin_amdgcn_s_memtime();)
         rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt);
+        RT_LSEG(const unsigned long long tp = __builtin_amdgcn_s_memtime() - tp0;
+                if (level == 0) {
+                    sg_cam += tp;
+                    sg_vcam += P.nodes + ((unsigned long long)P.leaves << 32);
+                } else {
+                    sg_mir += tp;
+                })
         const bool hit = alive && P.best_rank >= 0;
         if (alive && !hit) term = rtt::ld3(F.bg255);  // :310-311
         rts::Surface sf;
@@ -134,6 +155,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
             rtt::RayCtx rs;
             rtt::setup_ray(rs, sr.o, sr.dir);
             rtp::PacketLane Q;
+            RT_LSEG(const unsigned long long tq0 = __builtin_amdgcn_s_memtime();)
             if (STASH > 0) {
                 volatile float *vs = stash_mem + rtt::lane_id();
                 const float v[18] = {col.x, col.y, col.z, lit.x, lit.y, lit.z, term.x, term.y, term.z,
@@ -153,6 +175,8 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
             } else {
                 rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
             }
+            RT_LSEG(sg_sh += __builtin_amdgcn_s_memtime() - tq0;
+                    sg_vsh += Q.nodes + ((unsigned long long)Q.leaves << 32);)
             if (trace && Q.best_rank != 1) col = lit;
         }
         bool mirror = false;
@@ -191,6 +215,21 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         const unsigned e = c ? 31u - __clz(c) : 0u;
         F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
     }
+#ifdef RT_SEG_PROFILE
+    for (int off = 32; off > 0; off >>= 1) {  // lane 0's copies may be stale if it sat out a packet
+        sg_vcam = max(sg_vcam, (unsigned long long)__shfl_xor((long long)sg_vcam, off));
+        sg_vsh = max(sg_vsh, (unsigned long long)__shfl_xor((long long)sg_vsh, off));
+    }
+    if (lane2 == 0) {  // the clocks are wave-uniform
+        unsigned long long *ctr = F.counters + (size_t)(blockIdx.x % kCounterSlots) * kCounterWords;
+        atomicAdd(ctr + 3, sg_vcam);
+        atomicAdd(ctr + 4, sg_cam);
+        atomicAdd(ctr + 5, sg_sh);
+        atomicAdd(ctr + 6, __builtin_amdgcn_s_memtime() - ts0);
+        atomicAdd(ctr + 7, sg_vsh);
+        (void)sg_mir;
+    }
+#endif
     if (F.wave_counts) {  // plain store, reduced after the launch (trace.hip wave_counts_kernel)
         unsigned sh = 0, rf = 0, mo = 0;
         if (__ballot((cnt.shadow | cnt.reflection | cnt.moot) != 0) != 0) {
