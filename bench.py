@@ -156,10 +156,12 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows):
     """The trace kernel instance a frame launches (rtk::launch_render_mega and
     lpt_prepare in csrc/trace.hip / csrc/rt_abi.cpp): the all-packet levels
     kernel for >= 16 spp, otherwise render_kernel<COUNT, SPLIT, DEEP, Q4, W> —
-    SPLIT when a frame or shard is small enough to split its slowest tiles
-    (<= 24,000 tiles, or <= 70,000 for sixteenth-waves only; the timed frames
-    are RT_FLAG_ASYNC, so whole frames do not split), Q4 for 2x2 spp, W the
-    waves per SIMD (5 for shards of <= 70,000 tiles and deep frames, else 6)."""
+    SPLIT when the frame splits its slowest tiles — shards always (quarter-
+    and sixteenth-waves up to 24,000 tiles, sixteenth-waves above), whole
+    frames when no frame of another stream runs beside them (lpt_prepare
+    overlapped_frame): the kernel-only frames below run back to back on one
+    stream, so they split — Q4 for 2x2 spp, W the waves per SIMD (5 for
+    shards of <= 70,000 tiles and deep frames, else 6)."""
     if mode == "packet":
         return "render_packet_kernel<false, true>"
     if mode == "wavefront":
@@ -172,7 +174,7 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows):
     th = 1 << (lg // 2) if ppw & (ppw - 1) == 0 else 1
     tw = ppw // th
     tiles = -(-res_x // tw) * -(-local_rows // th)
-    split = not deep and ((16 % spp == 0 and tiles <= 24000) or (4 % spp == 0 and tiles <= 70000))
+    split = not deep and ((16 % spp == 0 and tiles <= 24000) or 4 % spp == 0)
     waves = 5 if deep or (split and tiles <= 70000) else 6
     b = lambda v: "true" if v else "false"  # noqa: E731
     return (f"render_kernel<false, {b(split)}, {b(deep)}, {b(spp == 4 and tw == 4 and th == 4 and not deep)}, "

@@ -116,3 +116,18 @@ def test_failed_slab_leaves_no_copy_behind(gpu_ctx, rt, fail_slab):
         assert lib.rt_debug_set(gpu_ctx.h, rt.abi.RT_DEBUG_FAIL_SLAB, -1) == 0
     again, _ = gpu_ctx.render(fr.camera, fr.plane, p)
     assert np.array_equal(again.view(np.uint32), good.view(np.uint32))
+
+
+def test_product_library_records_no_wave_clocks(gpu_ctx, rt):
+    """RT_DEBUG_WAVE_CLOCKS belongs to measuring builds (-DRT_WAVE_CLOCK): the
+    product library compiles no per-wave clock store and says so."""
+    import ctypes as C
+
+    lib = gpu_ctx.lib
+    assert lib.rt_debug_set(gpu_ctx.h, rt.abi.RT_DEBUG_WAVE_CLOCKS, 1) == rt.abi.RT_E_STATE
+    assert b"measuring" in lib.rt_last_error(gpu_ctx.h)
+    n = C.c_int64(-1)
+    buf = (C.c_uint32 * 4)()
+    assert lib.rt_debug_read(gpu_ctx.h, rt.abi.RT_DEBUG_WAVE_CLOCKS, C.cast(buf, C.c_void_p), 16,
+                             C.byref(n)) == rt.abi.RT_E_STATE
+    assert n.value == 0

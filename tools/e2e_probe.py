@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--frames", type=int, default=12)
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--variant", default="default")
+    ap.add_argument("--mapped", action="store_true", help="also render straight into mapped page-locked memory")
     a = ap.parse_args()
     rt = _rt_pkg.load()
     fr = rt.make(a.config)
@@ -72,6 +73,25 @@ def main():
             hs.copy_(dev)
             cs.append(time.perf_counter() - t0)
         out[f"copy_{kind}_ms"] = med(cs)
+    if a.mapped:
+        # the kernel stores straight into page-locked host memory over PCIe
+        # (rt_render_device with the pinned buffer's device address): no copy
+        import ctypes as C
+        lp = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+        hip = C.CDLL(lp)
+        pinned = torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True)
+        dptr = C.c_void_p()
+        rc = hip.hipHostGetDevicePointer(C.byref(dptr), C.c_void_p(pinned.data_ptr()), 0)
+        out["mapped_rc"] = rc
+        if rc == 0 and dptr.value:
+            ms = []
+            for _ in range(a.frames):
+                t0 = time.perf_counter()
+                st = ctx.render_device(fr.camera, fr.plane, p, dptr.value, nbytes)
+                ms.append(time.perf_counter() - t0)
+            out["render_mapped_ms"] = med(ms)
+            out["render_mapped_kernel_ms"] = round(st.kernel_ms, 4)
+            out["render_mapped_equal"] = bool(torch.equal(pinned, dev.cpu()))
     print(json.dumps(out), flush=True)
     ctx.close()
 

@@ -27,12 +27,11 @@ def seg_per_wave(st):
 def seg_levels_per_wave(st, waves):
     """RT_SEG_PROFILE words of render_levels_kernel -> per-wave averages."""
     w = max(1, waves)
-    vc, vs = st.box_tests, st.primary_scene_misses
+    vc, mir = st.box_tests, st.primary_scene_misses
     cam, sh, tot = st.triangle_tests, st.sphere_tests, st.shading_fetches
     return {"waves": w, "cam_nodes": round((vc & 0xffffffff) / w, 2), "cam_leaves": round((vc >> 32) / w, 2),
-            "shadow_nodes": round((vs & 0xffffffff) / w, 2), "shadow_leaves": round((vs >> 32) / w, 2),
-            "cam_cyc": round(cam / w), "shadow_cyc": round(sh / w), "total_cyc": round(tot / w),
-            "rest_cyc": round((tot - cam - sh) / w)}
+            "cam_cyc": round(cam / w), "shadow_cyc": round(sh / w), "mirror_cyc": round(mir / w),
+            "total_cyc": round(tot / w), "rest_cyc": round((tot - cam - sh - mir) / w)}
 
 
 def main():

@@ -48,6 +48,13 @@ for n in 2 4 8; do
   timeout -k 10 300 python bench.py --steps 100 --warmup 5 --no-cpu-baseline --sim-bands $n > gpurun_out/sb${n}_$tag.log 2>&1 || { echo sb$n-fail; exit 1; }
   timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --sim-bands $n --streams 1 > gpurun_out/sb${n}s1_$tag.log 2>&1 || { echo sb${n}s1-fail; exit 1; }
 done
+timeout -k 10 400 python tools/abx.py --config C5 --variants default,lv8 --rounds 4 --frames 3 \
+  > gpurun_out/abx_lv8_$tag.log 2>&1 || { echo abx-lv8-fail; tail gpurun_out/abx_lv8_$tag.log; exit 1; }
+grep variant gpurun_out/abx_lv8_$tag.log
+for fl in 8 0; do
+  timeout -k 10 200 python tools/e2e_probe.py --config C3 --frames 12 --flags $fl --mapped >> gpurun_out/e2e_$tag.log 2>&1 || { echo e2e-fail; tail gpurun_out/e2e_$tag.log; exit 1; }
+done
+echo e2e-ok
 for c in C4 C5; do
   timeout -k 10 300 python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --moving-frames 0 > gpurun_out/bench_${c}_$tag.log 2>&1 || { echo bench-$c-fail; exit 1; }
 done

@@ -51,6 +51,7 @@ def analyse(rec):
         "t_999pct_waves_done_us": round(int(order[int(0.999 * (len(order) - 1))]) * TICK_US, 2),
         "waves_running_at_90pct_span": int(np.sum((s <= 0.9 * span) & (e >= 0.9 * span))),
         "split_waves": int(np.sum(part >= 0)),
+        "top_waves_us": [round(int(x) * TICK_US, 1) for x in np.sort(dur)[::-1][:16]],
     }
 
 
@@ -61,7 +62,7 @@ def main():
     ap.add_argument("--bands", default="1,2,4,8")
     ap.add_argument("--frames", type=int, default=40)
     ap.add_argument("--async-frames", action="store_true",
-                    help="RT_FLAG_ASYNC frames (the frames-in-flight instance: whole frames do not split)")
+                    help="RT_FLAG_ASYNC frames back to back on one stream (they split like synchronous ones)")
     a = ap.parse_args()
     rt = _rt_pkg.load()
     fr = rt.make(a.config)

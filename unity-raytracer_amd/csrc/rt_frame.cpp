@@ -244,10 +244,13 @@ constexpr bool kSplitSync = false;  // measuring builds only
 #else
 constexpr bool kSplitSync = true;
 #endif
-// A synchronous frame (no RT_FLAG_ASYNC: Update() waits for it, RayTracingSetup.cs:
-// 171-199) has no next frame to hide its tail behind, so whole frames of any size
-// split their slowest 1/4096 into sixteenth-waves too: C3 single frame -9 % (0.290 ->
-// 0.264 ms, profiles/r04/abx_split); frames in flight keep the 70,000-tile limit.
+// A frame with no other frame beside it (synchronous: Update() waits for it,
+// RayTracingSetup.cs:171-199; or async frames on a single stream) has nothing to
+// hide its tail behind, so whole frames of any size split their slowest 1/4096
+// into sixteenth-waves too: C3 single frame -9 % (0.290 -> 0.264 ms,
+// profiles/r04/abx_split) — a C3 frame's slowest wave, one tile's mirror chains,
+// ran 0.32 ms against 0.24 ms for all the others (tools/wave_clock.py, r04i);
+// frames in flight on several streams keep the 70,000-tile limit.
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
 // kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
@@ -341,6 +344,18 @@ int record_async_end(rt_ctx *ctx) {
     return RT_OK;
 }
 
+// True when this frame may run beside another of the context's frames: an
+// RT_FLAG_ASYNC frame while a frame enqueued on another stream is pending
+// (since the last rt_finish), whose tiles then fill the GPU during this
+// frame's tail.  A frame with nothing beside it (synchronous, or async frames
+// on one stream) is its own critical path and splits its slowest tiles.
+static bool overlapped_frame(const rt_ctx *ctx, const rt_render_params *prm) {
+    if ((prm->flags & RT_FLAG_ASYNC) == 0) return false;
+    for (const auto &se : ctx->async_end)
+        if (se.first && se.first != ctx->stream) return true;
+    return false;
+}
+
 // Longest-first dispatch of a megakernel launch: picks the state of
 // (stream, slab), points F at the last measured order and decides whether
 // this launch measures costs (the caller sorts them after the launch).
@@ -402,7 +417,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
             F.split_tiles -= F.split16_tiles;
         }
     } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
-               (F.num_tiles <= kSplit16MaxTiles || (kSplitSync && (prm->flags & RT_FLAG_ASYNC) == 0))) {
+               (F.num_tiles <= kSplit16MaxTiles || (kSplitSync && !overlapped_frame(ctx, prm)))) {
         F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
     }
     // the split-tile instance's shadow occluder hints (packet.h packet_trace

@@ -52,8 +52,11 @@ struct SegClock {
 };
 
 // Ambient + every point light of one hit (RayTracingSetup.cs:320-356), shadow
-// rays traced per lane.
-template <bool COUNT>
+// rays traced per lane.  MOOT (the split-tile instances, whose waves hold a
+// frame's longest mirror chains): a moot shadow ray (shade.h same_bits) is not
+// traced, as in the packets — kept out of the common instance, where the test
+// added 25 spill sites.
+template <bool COUNT, bool MOOT = false>
 __device__ __forceinline__ f3 shade_hit(const SceneDev &S, const rts::Surface &sf, const rtt::Stack &st,
                                         Counts &cnt) {
     f3 col = rts::ambient(S, S.mats[sf.mat]);
@@ -64,6 +67,15 @@ __device__ __forceinline__ f3 shade_hit(const SceneDev &S, const rts::Surface &s
         rtt::setup_ray(rs, sr.o, sr.dir);
         float dt;
         int dr;
+        if (MOOT && !COUNT) {
+            const f3 lit = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+            if (rts::same_bits(lit, col)) {
+                cnt.moot++;
+                continue;
+            }
+            if (!rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) col = lit;
+            continue;
+        }
         if (rtt::traverse<true, COUNT>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, st, cnt)) continue;
         col = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
     }
@@ -165,7 +177,7 @@ __device__ __noinline__ f3 deep_chain(const SceneDev &S, const FrameDev &F, f3 o
 // c + km*(c' + km'*(...)) rounds exactly like the reference.  DEEP (frames with
 // MaxReflectionBounces > kMaxBounces only): a chain that outgrows the fold
 // stack continues in deep_chain.
-template <bool COUNT, bool DEEP>
+template <bool COUNT, bool DEEP, bool MOOT = false>
 __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F, f3 o, f3 d, int depth0,
                                            const rtt::Stack &st, Counts &cnt) {
     float fold_c[kMaxBounces][3];
@@ -187,7 +199,7 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
         if (DEEP && depth - depth0 == kMaxBounces && S.mats[sf.mat].ka_mirror.w != 0.0f && depth < F.max_bounces) {
             return deep_chain<COUNT>(S, F, o0, d0, depth0, o, d, st, cnt);
         }
-        const f3 col = shade_hit<COUNT>(S, sf, st, cnt);
+        const f3 col = shade_hit<COUNT, MOOT>(S, sf, st, cnt);
         const DevMaterial m = S.mats[sf.mat];
         if (m.ka_mirror.w != 0.0f && depth < F.max_bounces) {  // :358-363
             fold_c[depth - depth0][0] = col.x; fold_c[depth - depth0][1] = col.y; fold_c[depth - depth0][2] = col.z;
@@ -206,15 +218,83 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 }
 
 
+// The mirror chain below a first hit (levels 1, 2, ...) as wave packets: each
+// level's closest-hit rays, then their shadow rays, traced by the lanes still
+// bouncing together, as render_levels_kernel traces every level.  For the
+// split waves (one pixel's samples, or a 2x2-pixel block's): their chains stay
+// coherent, they are a small frame's longest waves, and a packet fetches each
+// node once by scalar load instead of once per lane.  Called by every lane with
+// a first hit (alive: its hit is a mirror below MaxReflectionBounces, o / d the
+// reflected ray); the same arithmetic, counts and back-to-front fold as
+// shade_levels from depth 1.
+__device__ __forceinline__ f3 mirror_packets(const SceneDev &S, const FrameDev &F, bool alive, f3 o, f3 d,
+                                             int *wstack, Counts &cnt) {
+    float fold_c[kMaxBounces][3];
+    float fold_k[kMaxBounces][3];
+    int depth = 0;
+    f3 term = mk(0.0f, 0.0f, 0.0f);
+    for (int level = 1; __ballot(alive) != 0; ++level) {  // uniform over the calling lanes
+        rtt::RayCtx r;
+        rtt::setup_ray(r, o, d);
+        rtp::PacketLane P;
+        rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack, cnt);
+        const bool hit = alive && P.best_rank >= 0;
+        if (alive && !hit) term = rtt::ld3(F.bg255);  // :310-311
+        rts::Surface sf;
+        f3 col = mk(0.0f, 0.0f, 0.0f);
+        int mat = 0;
+        if (hit) {
+            sf = rts::surface(S, o, d, P.best_t, P.best_rank);
+            mat = sf.mat;
+            col = rts::ambient(S, S.mats[mat]);
+        } else {
+            sf.p = sf.n = sf.view = mk(0.0f, 0.0f, 1.0f);
+            sf.mat = 0;
+        }
+        for (int l = 0; l < S.num_lights; ++l) {  // :327-356
+            const DevLight Lt = S.lights[l];
+            const rts::ShadowRay sr = rts::shadow_ray(sf, Lt);
+            if (hit) cnt.shadow++;
+            const f3 lit = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
+            const bool trace = hit && !rts::same_bits(lit, col);  // a moot shadow ray is not traced
+            cnt.moot += hit && !trace;
+            rtt::RayCtx rs;
+            rtt::setup_ray(rs, sr.o, sr.dir);
+            rtp::PacketLane Q;
+            rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
+            if (trace && Q.best_rank != 1) col = lit;
+        }
+        bool mirror = false;
+        if (hit) {
+            const DevMaterial m = S.mats[mat];
+            mirror = m.ka_mirror.w != 0.0f && level < F.max_bounces;  // :358
+            if (mirror) {
+                fold_c[depth][0] = col.x; fold_c[depth][1] = col.y; fold_c[depth][2] = col.z;
+                fold_k[depth][0] = m.km.x; fold_k[depth][1] = m.km.y; fold_k[depth][2] = m.km.z;
+                rts::reflect(sf, o, d);
+                ++depth;
+                cnt.reflection++;
+            } else {
+                term = col;
+            }
+        }
+        alive = mirror;
+    }
+    for (int k = depth - 1; k >= 0; --k)
+        term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
+    return term;
+}
+
 // Shade (RayTracingSetup.cs:304-366) of one camera sample.  The first hit is
 // traced and shaded with wave packets (camera rays of a tile, then their
 // shadow rays to each light: packet.h, scalar node fetches); the mirror
 // chain below it (a few percent of samples) runs per lane (shade_levels).
 // The counting launch keeps the per-ray traversal's canonical counts.
-template <bool COUNT, bool DEEP, bool HINT>
+template <bool COUNT, bool DEEP, bool HINT, bool MOOT>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
                                          int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs, int tile,
-                                         float *stash) {
+                                         float *stash, bool pchain) {
+    (void)pchain;
     (void)stash;
     (void)sg;
     (void)tile;
@@ -288,11 +368,23 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     }
 #undef RT_LIT
     const DevMaterial m = S.mats[sf.mat];
+#ifdef RT_EXP_PCHAIN
+    if ((RT_EXP_PCHAIN == 5 ? HINT : MOOT) && !COUNT && !DEEP && pchain) {  // a split wave: the chain as packets
+        const bool mir = m.ka_mirror.w != 0.0f && 0 < F.max_bounces;  // :358-363
+        f3 ro = o, rd = d;
+        if (mir) {
+            cnt.reflection++;
+            rts::reflect(sf, ro, rd);
+        }
+        const f3 below = mirror_packets(S, F, mir, ro, rd, wstack, cnt);
+        return mir ? col + mk(m.km.x, m.km.y, m.km.z) * below : col;
+    }
+#endif
     if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363
         cnt.reflection++;
         f3 ro, rd;
         rts::reflect(sf, ro, rd);
-        const f3 below = shade_levels<COUNT, DEEP>(S, F, ro, rd, 1, st, cnt);
+        const f3 below = shade_levels<COUNT, DEEP, MOOT>(S, F, ro, rd, 1, st, cnt);
         return col + mk(m.km.x, m.km.y, m.km.z) * below;
     }
     return col;
@@ -311,6 +403,9 @@ constexpr int kMkMinWaves = RT_EXP_MKWAVES;  // measuring builds only
 constexpr int kMkMinWaves = 6;
 #endif
 constexpr int kMkMinWavesShard = 5;
+// LDS stack entries of the 5-wave instances: 24 (a 1/2 C3 shard, single frame:
+// 0.199 ms with 16 entries, 0.186 with 24, r04i; the LDS does not bind at five waves)
+constexpr int kStackShard = 24;
 constexpr int kShardTiles = 70000;  // rt_frame.cpp kSplit16MaxTiles: a 1/2 shard of 1080p at 4 spp
 // Waves per megakernel workgroup.  A workgroup's slot is recycled only when
 // all of its waves are done, and path lengths vary a lot between tiles, so
@@ -325,7 +420,7 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // one of the four (pshift 4: 16 lanes) or sixteen (pshift 2: 4 lanes) waves
 // an expensive tile is split into.
 // Returns true when the tile was answered by the sky test (no exact rays).
-template <bool COUNT, bool DEEP, bool Q4, bool HINT>
+template <bool COUNT, bool DEEP, bool Q4, bool HINT, bool MOOT>
 __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
                                             SegClock &sg, float *stash) {
@@ -358,7 +453,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
                 cnt.scene_miss +=
                     !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
             }
-            color = shade_path<COUNT, DEEP, HINT>(S, F, o, d, st, wstack, cnt, sg, cs, tile, stash);
+            color = shade_path<COUNT, DEEP, HINT, MOOT>(S, F, o, d, st, wstack, cnt, sg, cs, tile, stash, part >= 0);
         }
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
@@ -388,7 +483,10 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
 // 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel).
 template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false, int W = kMkMinWaves>
 __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, FrameDev F) {
-    __shared__ int stack_mem[kMkWaves * kStackSize * kWaveSize];
+    // the per-lane LDS stack: kStackSize entries where six waves per SIMD must
+    // fit the CU's LDS, kStackShard at five (fewer overflows to scratch)
+    constexpr int SS = W >= 6 ? kStackSize : kStackShard;
+    __shared__ int stack_mem[kMkWaves * SS * kWaveSize];
     __shared__ int wstack_mem[kMkWaves * rtp::kWaveStack];
 #ifdef RT_EXP_MKSTASH
     __shared__ float stash_mem[kMkWaves * 15 * kWaveSize];
@@ -399,8 +497,8 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     const int lane = threadIdx.x & 63;
     // wave-uniform (an SGPR; with one-wave workgroups simply the block index)
     const int wave = kMkWaves == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem + wave * kStackSize * kWaveSize, ovf};  // + lane per query (traverse)
+    int ovf[kStackTotal - SS];
+    const rtt::Stack st{stack_mem + wave * SS * kWaveSize, ovf, SS};  // + lane per query (traverse)
     int *const wstack = wstack_mem + wave * rtp::kWaveStack;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int wid = blockIdx.x * kMkWaves + wave;
@@ -427,6 +525,10 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     } else {
         idx = wid - 15 * split16 - 3 * split;
     }
+#ifdef RT_EXP_SPLITPRIO
+    // measuring builds: the split waves (a frame's longest chains) at a higher issue priority
+    if (SPLIT && part >= 0) __builtin_amdgcn_s_setprio(RT_EXP_SPLITPRIO);
+#endif
     // the tile index is wave-uniform and kept in an SGPR: the slot -> pixel
     // integer math runs on the scalar unit and nothing of it is spilled
     int tile = idx;
@@ -438,7 +540,11 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     SegClock sg = {0ull, 0ull, 0ull, 0ull};
     RT_SEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();)
-    const bool sky = render_tile<COUNT, DEEP, Q4, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, stash);
+    // the shadow occluder hints (packet.h HINT) pay off in small frames only:
+    // the 5-wave split instance (row shards), not the whole-frame one
+    constexpr bool HINT = SPLIT && W < 6;
+    const bool sky = render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg,
+                                                               stash);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order

@@ -64,7 +64,7 @@ constexpr int kLvStashHigh = 0;
 // RT_SEG_PROFILE (profiling builds only): per-wave shader-clock time of the
 // camera packets (level 0), the shadow packets (every level), the mirror-ray
 // packets (levels >= 1) and the whole tile, plus the wave-level node / leaf
-// visits of the camera and shadow packets, summed into the (otherwise unused,
+// visits of the camera packets, summed into the (otherwise unused,
 // non-counting) test-counter words 3-7 (tools/probe.py reads them).
 #ifdef RT_SEG_PROFILE
 #define RT_LSEG(...) __VA_ARGS__
@@ -226,8 +226,8 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         atomicAdd(ctr + 4, sg_cam);
         atomicAdd(ctr + 5, sg_sh);
         atomicAdd(ctr + 6, __builtin_amdgcn_s_memtime() - ts0);
-        atomicAdd(ctr + 7, sg_vsh);
-        (void)sg_mir;
+        atomicAdd(ctr + 7, sg_mir);
+        (void)sg_vsh;
     }
 #endif
     if (F.wave_counts) {  // plain store, reduced after the launch (trace.hip wave_counts_kernel)

@@ -103,6 +103,7 @@ struct Trav {
 struct Stack {
     int *lds;
     int *ovf;
+    int n = rtd::kStackSize;  // entries in LDS (a constant of the kernel instance)
 };
 
 // Overflow accesses are volatile so the compiler never folds the LDS and
@@ -110,10 +111,10 @@ struct Stack {
 typedef volatile int ovf_int;
 
 __device__ __forceinline__ void push(Trav &t, const Stack &st, int v) {
-    if (t.sp < rtd::kStackSize)
+    if (t.sp < st.n)
         st.lds[t.sp * kWaveSize] = v;
     else
-        ((ovf_int *)st.ovf)[t.sp - rtd::kStackSize] = v;
+        ((ovf_int *)st.ovf)[t.sp - st.n] = v;
     ++t.sp;
 }
 
@@ -121,10 +122,10 @@ __device__ __forceinline__ void push(Trav &t, const Stack &st, int v) {
 __device__ __forceinline__ bool pop(Trav &t, const Stack &st) {
     if (t.sp == 0) return false;
     --t.sp;
-    if (t.sp < rtd::kStackSize)
+    if (t.sp < st.n)
         t.node = st.lds[t.sp * kWaveSize];
     else
-        t.node = ((ovf_int *)st.ovf)[t.sp - rtd::kStackSize];
+        t.node = ((ovf_int *)st.ovf)[t.sp - st.n];
     return true;
 }
 
@@ -348,7 +349,7 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
         if (k0 != INFINITY) {
             // push the other hit children far-first: bottom..top = c_{h-1} .. c1
             const int h = 1 + (k1 != INFINITY) + (k2 != INFINITY) + (k3 != INFINITY);
-            if (t.sp + 3 <= rtd::kStackSize) {
+            if (t.sp + 3 <= st.n) {
                 // branch-free: three unconditional LDS writes, sp advances by h-1
                 const int s0 = h == 4 ? c3 : (h == 3 ? c2 : c1);
                 const int s1 = h == 4 ? c2 : c1;
