@@ -218,73 +218,6 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 }
 
 
-// The mirror chain below a first hit (levels 1, 2, ...) as wave packets: each
-// level's closest-hit rays, then their shadow rays, traced by the lanes still
-// bouncing together, as render_levels_kernel traces every level.  For the
-// split waves (one pixel's samples, or a 2x2-pixel block's): their chains stay
-// coherent, they are a small frame's longest waves, and a packet fetches each
-// node once by scalar load instead of once per lane.  Called by every lane with
-// a first hit (alive: its hit is a mirror below MaxReflectionBounces, o / d the
-// reflected ray); the same arithmetic, counts and back-to-front fold as
-// shade_levels from depth 1.
-__device__ __forceinline__ f3 mirror_packets(const SceneDev &S, const FrameDev &F, bool alive, f3 o, f3 d,
-                                             int *wstack, Counts &cnt) {
-    float fold_c[kMaxBounces][3];
-    float fold_k[kMaxBounces][3];
-    int depth = 0;
-    f3 term = mk(0.0f, 0.0f, 0.0f);
-    for (int level = 1; __ballot(alive) != 0; ++level) {  // uniform over the calling lanes
-        rtt::RayCtx r;
-        rtt::setup_ray(r, o, d);
-        rtp::PacketLane P;
-        rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack, cnt);
-        const bool hit = alive && P.best_rank >= 0;
-        if (alive && !hit) term = rtt::ld3(F.bg255);  // :310-311
-        rts::Surface sf;
-        f3 col = mk(0.0f, 0.0f, 0.0f);
-        int mat = 0;
-        if (hit) {
-            sf = rts::surface(S, o, d, P.best_t, P.best_rank);
-            mat = sf.mat;
-            col = rts::ambient(S, S.mats[mat]);
-        } else {
-            sf.p = sf.n = sf.view = mk(0.0f, 0.0f, 1.0f);
-            sf.mat = 0;
-        }
-        for (int l = 0; l < S.num_lights; ++l) {  // :327-356
-            const DevLight Lt = S.lights[l];
-            const rts::ShadowRay sr = rts::shadow_ray(sf, Lt);
-            if (hit) cnt.shadow++;
-            const f3 lit = col + rts::light_term(S, sf, S.mats[mat], Lt, sr);
-            const bool trace = hit && !rts::same_bits(lit, col);  // a moot shadow ray is not traced
-            cnt.moot += hit && !trace;
-            rtt::RayCtx rs;
-            rtt::setup_ray(rs, sr.o, sr.dir);
-            rtp::PacketLane Q;
-            rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt);
-            if (trace && Q.best_rank != 1) col = lit;
-        }
-        bool mirror = false;
-        if (hit) {
-            const DevMaterial m = S.mats[mat];
-            mirror = m.ka_mirror.w != 0.0f && level < F.max_bounces;  // :358
-            if (mirror) {
-                fold_c[depth][0] = col.x; fold_c[depth][1] = col.y; fold_c[depth][2] = col.z;
-                fold_k[depth][0] = m.km.x; fold_k[depth][1] = m.km.y; fold_k[depth][2] = m.km.z;
-                rts::reflect(sf, o, d);
-                ++depth;
-                cnt.reflection++;
-            } else {
-                term = col;
-            }
-        }
-        alive = mirror;
-    }
-    for (int k = depth - 1; k >= 0; --k)
-        term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
-    return term;
-}
-
 // Shade (RayTracingSetup.cs:304-366) of one camera sample.  The first hit is
 // traced and shaded with wave packets (camera rays of a tile, then their
 // shadow rays to each light: packet.h, scalar node fetches); the mirror
@@ -293,8 +226,7 @@ __device__ __forceinline__ f3 mirror_packets(const SceneDev &S, const FrameDev &
 template <bool COUNT, bool DEEP, bool HINT, bool MOOT>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
                                          int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs, int tile,
-                                         float *stash, bool pchain) {
-    (void)pchain;
+                                         float *stash) {
     (void)stash;
     (void)sg;
     (void)tile;
@@ -368,18 +300,6 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     }
 #undef RT_LIT
     const DevMaterial m = S.mats[sf.mat];
-#ifdef RT_EXP_PCHAIN
-    if ((RT_EXP_PCHAIN == 5 ? HINT : MOOT) && !COUNT && !DEEP && pchain) {  // a split wave: the chain as packets
-        const bool mir = m.ka_mirror.w != 0.0f && 0 < F.max_bounces;  // :358-363
-        f3 ro = o, rd = d;
-        if (mir) {
-            cnt.reflection++;
-            rts::reflect(sf, ro, rd);
-        }
-        const f3 below = mirror_packets(S, F, mir, ro, rd, wstack, cnt);
-        return mir ? col + mk(m.km.x, m.km.y, m.km.z) * below : col;
-    }
-#endif
     if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363
         cnt.reflection++;
         f3 ro, rd;
@@ -453,7 +373,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
                 cnt.scene_miss +=
                     !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
             }
-            color = shade_path<COUNT, DEEP, HINT, MOOT>(S, F, o, d, st, wstack, cnt, sg, cs, tile, stash, part >= 0);
+            color = shade_path<COUNT, DEEP, HINT, MOOT>(S, F, o, d, st, wstack, cnt, sg, cs, tile, stash);
         }
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);

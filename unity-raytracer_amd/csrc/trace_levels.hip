@@ -23,15 +23,15 @@ using rtt::Counts;
 namespace {
 
 // Waves per SIMD the register budget must allow: 6 (80 VGPRs, fewer spills in
-// the level loop) for up to 16 spp, 7 (72 VGPRs) above.  Measured (round 3,
+// the level loop) for up to 16 spp, 8 (64 VGPRs) above.  Measured (round 3,
 // interleaved A/B): C4 (16 spp, depth 8) 6 waves -5 % single frame / -8 %
 // frames in flight against 7; C5 (64 spp, depth 16) 6 waves +2 %, 5 waves
-// +6 %.
+// +6 % against 7; 8 waves -1.1 % against 7 (r04l).
 constexpr int kLvWavesLowSpp = 6;
 #ifdef RT_EXP_LVHIGH
 constexpr int kLvWavesHighSpp = RT_EXP_LVHIGH;  // measuring builds only
 #else
-constexpr int kLvWavesHighSpp = 7;
+constexpr int kLvWavesHighSpp = 8;
 #endif
 
 // Level-synchronous all-packet megakernel (the default non-counting path on
@@ -39,21 +39,21 @@ constexpr int kLvWavesHighSpp = 7;
 // advances level by level for the whole wave, and every level's rays — the
 // camera rays, the mirror rays of the lanes still bouncing, and each level's
 // shadow rays — are traced as wave packets (packet.h).  Without a per-lane
-// traversal the kernel needs no LDS lane stack and 72-80 VGPRs (7 or 6
+// traversal the kernel needs no LDS lane stack and 64-80 VGPRs (8 or 6
 // waves/SIMD, kLvWaves*); the mirror fold (c + km*(...), evaluated back to front as the
 // recursion rounds) lives in scratch and is touched only by mirror lanes.
-// Same arithmetic per sample as render_kernel.  The camera packets start at
-// the root: the top-level cut start (packet.h cut_select) measured +5 % on C4
-// and +15 % on C5 here (per-wave selection cost on 1- and 4-pixel tiles, more
-// spills in the level loop; round 3, tools/exp/ab_cfg.sh).
+// Same arithmetic per sample as render_kernel.  The <= 16-spp instance's
+// camera packets start below the top-level cut (below); round 3 measured that
+// start +5 % on C4 before the LDS stash of the shadow-packet state freed the
+// registers it needs.
 
 // Lane state kept in LDS across a shadow packet (per instance): the 6-wave
 // (<= 16 spp) instance stashes the hit (point, normal, view), the colour with
 // and without the light and the mirror chain's term — 18 floats a lane, 4.5
 // KB a wave — instead of spilling them around the packet loop: C4 HBM writes
 // 4.40 -> 0.30 GB per launch, kernel -3 % single frame / -5 % frames in flight
-// (profiles/r04/).  The 7-wave (64 spp) instance keeps none: at 28 waves per
-// CU the LDS would cap it at 6 (C5 +6 %, and +3 % at 6 waves/SIMD).
+// (profiles/r04/).  The 64-spp instance keeps none: a stash measured C5 +6 %
+// at 7 waves/SIMD and +3 % at 6 (r04f).
 constexpr int kXcdStripeRows = 4;  // tile rows per XCD stripe (render_levels_kernel dispatch)
 
 #ifdef RT_EXP_LVSTASH_HI
@@ -118,12 +118,24 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         }
         if (sky) alive = false;
     }
+    // The <= 16-spp instance's camera packets start below the top-level cut
+    // (packet.h cut_select, as render_kernel's): C4 -5.6 % single frame and
+    // frames in flight (r04l).  Not at 64 spp: a one-pixel tile's frustum
+    // touches most of C5's heavily overlapping top-level boxes, and every
+    // waiting entry costs a scalar round trip when popped: C5 +43 %.
+    constexpr bool CUT = MIN_WAVES == kLvWavesLowSpp;
+    rtp::CutStart cs = {0, 0, 0, -1};
+    if (CUT && F.cut_test && __ballot(alive) != 0) {  // every lane executes here
+        const rtp::CutLane cl = rtp::cut_load(S);
+        cs = rtp::cut_select(S, F, rts::tile_rect(F, tile), wstack_mem, &cl);
+    }
     for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
         rtt::RayCtx r;
         rtt::setup_ray(r, o, d);
         rtp::PacketLane P;
         RT_LSEG(const unsigned long long tp0 = __builtin_amdgcn_s_memtime();)
-        rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt);
+        rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt,
+                                        CUT && level == 0 ? &cs : nullptr);
         RT_LSEG(const unsigned long long tp = __builtin_amdgcn_s_memtime() - tp0;
                 if (level == 0) {
                     sg_cam += tp;
