@@ -27,11 +27,12 @@ def seg_per_wave(st):
 def seg_levels_per_wave(st, waves):
     """RT_SEG_PROFILE words of render_levels_kernel -> per-wave averages."""
     w = max(1, waves)
-    vc, mir = st.box_tests, st.primary_scene_misses
+    se, mir = st.box_tests, st.primary_scene_misses
+    setup, epi = (se & 0xffffffff) * 16, (se >> 32) * 16
     cam, sh, tot = st.triangle_tests, st.sphere_tests, st.shading_fetches
-    return {"waves": w, "cam_nodes": round((vc & 0xffffffff) / w, 2), "cam_leaves": round((vc >> 32) / w, 2),
-            "cam_cyc": round(cam / w), "shadow_cyc": round(sh / w), "mirror_cyc": round(mir / w),
-            "total_cyc": round(tot / w), "rest_cyc": round((tot - cam - sh - mir) / w)}
+    return {"waves": w, "setup_cyc": round(setup / w), "cam_cyc": round(cam / w), "shadow_cyc": round(sh / w),
+            "mirror_cyc": round(mir / w), "epilogue_cyc": round(epi / w), "total_cyc": round(tot / w),
+            "shading_cyc": round((tot - setup - epi - cam - sh - mir) / w)}
 
 
 def main():

@@ -62,10 +62,10 @@ constexpr int kLvStashHigh = RT_EXP_LVSTASH_HI;  // measuring builds only (0, 9 
 constexpr int kLvStashHigh = 0;
 #endif
 // RT_SEG_PROFILE (profiling builds only): per-wave shader-clock time of the
-// camera packets (level 0), the shadow packets (every level), the mirror-ray
-// packets (levels >= 1) and the whole tile, plus the wave-level node / leaf
-// visits of the camera packets, summed into the (otherwise unused,
-// non-counting) test-counter words 3-7 (tools/probe.py reads them).
+// setup, the camera packets (level 0), the shadow packets (every level, with
+// their LDS stash), the mirror-ray packets (levels >= 1), the epilogue and the
+// whole tile, summed into the (otherwise unused, non-counting) test-counter
+// words 3-7 (tools/probe.py reads them); the rest is per-level shading.
 #ifdef RT_SEG_PROFILE
 #define RT_LSEG(...) __VA_ARGS__
 #else
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     int tile = __builtin_amdgcn_readfirstlane(wid);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     RT_LSEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
-            unsigned long long sg_cam = 0, sg_sh = 0, sg_mir = 0, sg_vcam = 0, sg_vsh = 0;)
+            unsigned long long sg_cam = 0, sg_sh = 0, sg_mir = 0, sg_setup = 0;)
     float fold_c[kMaxBounces][3];
     float fold_k[kMaxBounces][3];
     int depth = 0;
@@ -129,6 +129,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         const rtp::CutLane cl = rtp::cut_load(S);
         cs = rtp::cut_select(S, F, rts::tile_rect(F, tile), wstack_mem, &cl);
     }
+    RT_LSEG(sg_setup = __builtin_amdgcn_s_memtime() - ts0;)
     for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
         rtt::RayCtx r;
         rtt::setup_ray(r, o, d);
@@ -137,12 +138,8 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt,
                                         CUT && level == 0 ? &cs : nullptr);
         RT_LSEG(const unsigned long long tp = __builtin_amdgcn_s_memtime() - tp0;
-                if (level == 0) {
-                    sg_cam += tp;
-                    sg_vcam += P.nodes + ((unsigned long long)P.leaves << 32);
-                } else {
-                    sg_mir += tp;
-                })
+                if (level == 0) sg_cam += tp;
+                else sg_mir += tp;)
         const bool hit = alive && P.best_rank >= 0;
         if (alive && !hit) term = rtt::ld3(F.bg255);  // :310-311
         rts::Surface sf;
@@ -187,8 +184,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
             } else {
                 rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
             }
-            RT_LSEG(sg_sh += __builtin_amdgcn_s_memtime() - tq0;
-                    sg_vsh += Q.nodes + ((unsigned long long)Q.leaves << 32);)
+            RT_LSEG(sg_sh += __builtin_amdgcn_s_memtime() - tq0;)
             if (trace && Q.best_rank != 1) col = lit;
         }
         bool mirror = false;
@@ -207,6 +203,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         }
         alive = mirror;
     }
+    RT_LSEG(const unsigned long long te0 = __builtin_amdgcn_s_memtime();)
     for (int k = depth - 1; k >= 0; --k)
         term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
     // lane ids recomputed (rtt::lane_id), not kept live across the levels
@@ -228,18 +225,15 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
     }
 #ifdef RT_SEG_PROFILE
-    for (int off = 32; off > 0; off >>= 1) {  // lane 0's copies may be stale if it sat out a packet
-        sg_vcam = max(sg_vcam, (unsigned long long)__shfl_xor((long long)sg_vcam, off));
-        sg_vsh = max(sg_vsh, (unsigned long long)__shfl_xor((long long)sg_vsh, off));
-    }
     if (lane2 == 0) {  // the clocks are wave-uniform
+        const unsigned long long te1 = __builtin_amdgcn_s_memtime();
         unsigned long long *ctr = F.counters + (size_t)(blockIdx.x % kCounterSlots) * kCounterWords;
-        atomicAdd(ctr + 3, sg_vcam);
+        // setup (slot, sky test, primary rays, cut) and epilogue (fold, sample sum, store) in 16-cycle units
+        atomicAdd(ctr + 3, (sg_setup >> 4) | (((te1 - te0) >> 4) << 32));
         atomicAdd(ctr + 4, sg_cam);
         atomicAdd(ctr + 5, sg_sh);
-        atomicAdd(ctr + 6, __builtin_amdgcn_s_memtime() - ts0);
+        atomicAdd(ctr + 6, te1 - ts0);
         atomicAdd(ctr + 7, sg_mir);
-        (void)sg_vsh;
     }
 #endif
     if (F.wave_counts) {  // plain store, reduced after the launch (trace.hip wave_counts_kernel)
