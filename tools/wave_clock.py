@@ -52,6 +52,7 @@ def analyse(rec):
         "waves_running_at_90pct_span": int(np.sum((s <= 0.9 * span) & (e >= 0.9 * span))),
         "split_waves": int(np.sum(part >= 0)),
         "top_waves_us": [round(int(x) * TICK_US, 1) for x in np.sort(dur)[::-1][:16]],
+        "top_waves_split": [int(part[i]) for i in np.argsort(dur)[::-1][:16]],
     }
 
 

@@ -239,6 +239,15 @@ constexpr int kSplit16MaxTiles = RT_EXP_SPLIT16MAX;  // measuring builds only
 constexpr int kSplit16MaxTiles = 70000;
 #endif
 constexpr int kSplit16DivLarge = 4096;
+// ... and a shard of that size with no other frame beside it (lpt_prepare
+// overlapped_frame: a synchronous Update() frame of one rank) its slowest
+// 1/1024: a 1/2 C3 shard's single frame -10.6 %, frames in flight +-0 (r04n;
+// its slowest waves were whole tiles of ~190 us against a 148-us dispatch).
+#ifdef RT_EXP_SPLIT16LONE
+constexpr int kSplit16DivLone = RT_EXP_SPLIT16LONE;  // measuring builds only
+#else
+constexpr int kSplit16DivLone = 1024;
+#endif
 #ifdef RT_EXP_NOSYNCSPLIT
 constexpr bool kSplitSync = false;  // measuring builds only
 #else
@@ -418,7 +427,8 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         }
     } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
                (F.num_tiles <= kSplit16MaxTiles || (kSplitSync && !overlapped_frame(ctx, prm)))) {
-        F.split16_tiles = std::max(1, F.num_tiles / kSplit16DivLarge);
+        const bool lone_shard = F.num_tiles <= kSplit16MaxTiles && !overlapped_frame(ctx, prm);
+        F.split16_tiles = std::max(1, F.num_tiles / (lone_shard ? kSplit16DivLone : kSplit16DivLarge));
     }
     // the split-tile instance's shadow occluder hints (packet.h packet_trace
     // HINT): leaf refs of the tree they were recorded on, so cleared whenever

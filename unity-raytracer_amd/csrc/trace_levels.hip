@@ -52,14 +52,16 @@ constexpr int kLvWavesHighSpp = 8;
 // and without the light and the mirror chain's term — 18 floats a lane, 4.5
 // KB a wave — instead of spilling them around the packet loop: C4 HBM writes
 // 4.40 -> 0.30 GB per launch, kernel -3 % single frame / -5 % frames in flight
-// (profiles/r04/).  The 64-spp instance keeps none: a stash measured C5 +6 %
-// at 7 waves/SIMD and +3 % at 6 (r04f).
+// (profiles/r04/).  The 64-spp instance (8 waves/SIMD: 4.6 KB of LDS a wave
+// fits 32 waves per CU) stashes 15 floats — all but the view vector: C5 HBM
+// writes 19.6 -> 10.6 GB and reads 9.2 -> 3.4 GB per launch at the same time
+// (r04n; 9 floats +1.3 %, 15 at 7 waves +2.4 %, 18 at 7 waves +6 %).
 constexpr int kXcdStripeRows = 4;  // tile rows per XCD stripe (render_levels_kernel dispatch)
 
 #ifdef RT_EXP_LVSTASH_HI
-constexpr int kLvStashHigh = RT_EXP_LVSTASH_HI;  // measuring builds only (0, 9 or 18)
+constexpr int kLvStashHigh = RT_EXP_LVSTASH_HI;  // measuring builds only (0, 9, 15 or 18)
 #else
-constexpr int kLvStashHigh = 0;
+constexpr int kLvStashHigh = 15;
 #endif
 // RT_SEG_PROFILE (profiling builds only): per-wave shader-clock time of the
 // setup, the camera packets (level 0), the shadow packets (every level, with
@@ -176,11 +178,11 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
                 col = mk(vs[0], vs[64], vs[128]);
                 lit = mk(vs[192], vs[256], vs[320]);
                 term = mk(vs[384], vs[448], vs[512]);
-                if (STASH >= 18) {
+                if (STASH >= 15) {
                     sf.p = mk(vs[576], vs[640], vs[704]);
                     sf.n = mk(vs[768], vs[832], vs[896]);
-                    sf.view = mk(vs[960], vs[1024], vs[1088]);
                 }
+                if (STASH >= 18) sf.view = mk(vs[960], vs[1024], vs[1088]);
             } else {
                 rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
             }
