@@ -92,11 +92,6 @@ __device__ __forceinline__ void packet_leaf_tris(const rtd::SceneDev &S, const R
     const rtd::TriRec *tb = S.tris + first;
     const rtd::TriRec t0 = rtt::cload(tb);
     const rtd::TriRec t1 = rtt::cload(tb + (count > 1 ? 1 : 0));
-#ifdef RT_EXP_LEAF4
-    // measuring builds: all four records in one round trip
-    const rtd::TriRec t2 = rtt::cload(tb + (count > 2 ? 2 : count - 1));
-    const rtd::TriRec t3 = rtt::cload(tb + (count > 3 ? 3 : count - 1));
-#endif
     const int gate = uni(__float_as_int(t0.p2.z));
     if (gate >= 0 && gate != wgate) {
         const rtd::MeshGate g = rtt::cload(S.gates + gate);
@@ -111,10 +106,8 @@ __device__ __forceinline__ void packet_leaf_tris(const rtd::SceneDev &S, const R
     if (packet_tri<ANY, COUNT>(r, L, d2, t0, cnt)) { L.live = false; return; }
     if (count > 1 && packet_tri<ANY, COUNT>(r, L, d2, t1, cnt)) { L.live = false; return; }
     if (count > 2) {
-#ifndef RT_EXP_LEAF4
         const rtd::TriRec t2 = rtt::cload(tb + 2);
         const rtd::TriRec t3 = rtt::cload(tb + (count > 3 ? 3 : 2));
-#endif
         if (packet_tri<ANY, COUNT>(r, L, d2, t2, cnt)) { L.live = false; return; }
         if (count > 3 && packet_tri<ANY, COUNT>(r, L, d2, t3, cnt)) { L.live = false; return; }
     }

@@ -225,9 +225,8 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 // The counting launch keeps the per-ray traversal's canonical counts.
 template <bool COUNT, bool DEEP, bool HINT, bool MOOT>
 __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f3 o, f3 d, const rtt::Stack &st,
-                                         int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs, int tile,
-                                         float *stash) {
-    (void)stash;
+                                         int *wstack, Counts &cnt, SegClock &sg, const rtp::CutStart &cs,
+                                         int tile) {
     (void)sg;
     (void)tile;
     if (COUNT || !S.bvh4) return shade_levels<COUNT, DEEP>(S, F, o, d, 0, st, cnt);
@@ -243,11 +242,7 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     int *const hints = HINT && F.shadow_hint ? F.shadow_hint + (size_t)tile * kHintLights : nullptr;
     int4 hv = make_int4(0, 0, 0, 0);
     if (HINT && hints) hv = rtt::cload(reinterpret_cast<const int4 *>(hints));
-#ifdef RT_EXP_MKSTASH
-    rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
-#else
     const rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
-#endif
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
         const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
@@ -262,43 +257,13 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         RT_SEG(const unsigned long long tw0 = __builtin_amdgcn_s_memtime();)
         const bool hl = HINT && hints && l < kHintLights;
         const int h = !hl ? 0 : l == 0 ? hv.x : l == 1 ? hv.y : l == 2 ? hv.z : hv.w;
-#ifdef RT_EXP_MKSTASH
-        // the hit's state lives in LDS across the shadow packet (volatile:
-        // reloaded after it, so its registers die at the store)
-        rts::Surface sfl = sf;
-        f3 litl = lit, coll = col;
-        {
-            volatile float *vs = stash + rtt::lane_id();
-            const float v[15] = {coll.x, coll.y, coll.z, litl.x, litl.y, litl.z, sfl.p.x, sfl.p.y, sfl.p.z,
-                                 sfl.n.x, sfl.n.y, sfl.n.z, sfl.view.x, sfl.view.y, sfl.view.z};
-#pragma unroll
-            for (int i = 0; i < 15; ++i) vs[i * kWaveSize] = v[i];
-        }
-#endif
         rtp::packet_trace<true, COUNT, HINT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr, h,
                                              hl ? hints + l : nullptr);
-#ifdef RT_EXP_MKSTASH
-        {
-            volatile float *vs = stash + rtt::lane_id();
-            coll = mk(vs[0], vs[64], vs[128]);
-            litl = mk(vs[192], vs[256], vs[320]);
-            sfl.p = mk(vs[384], vs[448], vs[512]);
-            sfl.n = mk(vs[576], vs[640], vs[704]);
-            sfl.view = mk(vs[768], vs[832], vs[896]);
-        }
-        sf = sfl;
-        col = coll;
-        const f3 lit2 = litl;
-#define RT_LIT lit2
-#else
-#define RT_LIT lit
-#endif
         RT_SEG(sg.shadow += __builtin_amdgcn_s_memtime() - tw0;
                sg.visits += Q.nodes + ((unsigned long long)Q.leaves << 32);)
         if (moot || Q.best_rank == 1) continue;
-        col = RT_LIT;
+        col = lit;
     }
-#undef RT_LIT
     const DevMaterial m = S.mats[sf.mat];
     if (m.ka_mirror.w != 0.0f && 0 < F.max_bounces) {  // :358-363
         cnt.reflection++;
@@ -343,7 +308,7 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 template <bool COUNT, bool DEEP, bool Q4, bool HINT, bool MOOT>
 __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
-                                            SegClock &sg, float *stash) {
+                                            SegClock &sg) {
     // the cut entries do not depend on the tile: their loads are issued first
     rtp::CutLane cl;
     if (!COUNT) cl = rtp::cut_load(S);
@@ -373,7 +338,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
                 cnt.scene_miss +=
                     !(S.has_prims && rtm::ref_slab(o, rg.inv(), rtt::ld3(S.scene_lo), rtt::ld3(S.scene_hi)));
             }
-            color = shade_path<COUNT, DEEP, HINT, MOOT>(S, F, o, d, st, wstack, cnt, sg, cs, tile, stash);
+            color = shade_path<COUNT, DEEP, HINT, MOOT>(S, F, o, d, st, wstack, cnt, sg, cs, tile);
         }
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
@@ -408,12 +373,6 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     constexpr int SS = W >= 6 ? kStackSize : kStackShard;
     __shared__ int stack_mem[kMkWaves * SS * kWaveSize];
     __shared__ int wstack_mem[kMkWaves * rtp::kWaveStack];
-#ifdef RT_EXP_MKSTASH
-    __shared__ float stash_mem[kMkWaves * 15 * kWaveSize];
-    float *const stash = stash_mem;  // (one wave per workgroup)
-#else
-    float *const stash = nullptr;
-#endif
     const int lane = threadIdx.x & 63;
     // wave-uniform (an SGPR; with one-wave workgroups simply the block index)
     const int wave = kMkWaves == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -445,10 +404,6 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     } else {
         idx = wid - 15 * split16 - 3 * split;
     }
-#ifdef RT_EXP_SPLITPRIO
-    // measuring builds: the split waves (a frame's longest chains) at a higher issue priority
-    if (SPLIT && part >= 0) __builtin_amdgcn_s_setprio(RT_EXP_SPLITPRIO);
-#endif
     // the tile index is wave-uniform and kept in an SGPR: the slot -> pixel
     // integer math runs on the scalar unit and nothing of it is spilled
     int tile = idx;
@@ -463,8 +418,7 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     // the shadow occluder hints (packet.h HINT) pay off in small frames only:
     // the 5-wave split instance (row shards), not the whole-frame one
     constexpr bool HINT = SPLIT && W < 6;
-    const bool sky = render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg,
-                                                               stash);
+    const bool sky = render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
