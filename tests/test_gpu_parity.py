@@ -308,9 +308,10 @@ def test_longest_first_order_is_invisible(gpu_ctx, rt):
 
 def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
     """Small frames (<= 24,000 tiles) run their slowest tiles, as measured by
-    the previous re-sort, as four quarter-waves (the slowest 1/2048 as sixteen
-    one-pixel waves): same bits and same ray counts as row-major whole-tile
-    frames, for a whole frame and for a row shard."""
+    the previous re-sort, as four quarter-waves (the slowest 1/2048 as 64
+    one-sample waves at 4 spp, whose pixel sums meet through write-through
+    stores and an arrival count): same bits and same ray counts as row-major
+    whole-tile frames, for a whole frame and for a row shard."""
     fr = rt.make("C3").with_resolution(640, 360)
     gpu_ctx.set_scene(fr.scene)
     for kw in ({}, dict(band_index=1, band_count=3, band_rows=8)):
@@ -324,11 +325,13 @@ def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
 
 def test_split_sixteenths_of_large_shards_is_invisible(gpu_ctx, rt):
     """Shards of 24,000-70,000 tiles (a 1/2 and a 1/4 shard of 1080p C3) run
-    only their slowest 1/4096 of tiles as sixteen one-pixel waves: same bits
-    and ray counts as row-major frames; the whole frame does not split."""
+    their slowest tiles finely split — synchronous (lone) frames their slowest
+    1/1024 as one-sample waves — and a whole synchronous 1080p frame its
+    slowest 1/4096 as one-pixel waves (the 6-wave split instance): same bits
+    and ray counts as row-major frames."""
     fr = rt.make("C3")
     gpu_ctx.set_scene(fr.scene)
-    for kw in (dict(band_index=0, band_count=2, band_rows=8), dict(band_index=3, band_count=4, band_rows=8)):
+    for kw in (dict(band_index=0, band_count=2, band_rows=8), dict(band_index=3, band_count=4, band_rows=8), {}):
         row, sr = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
         for _ in range(3):
             img, st = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))

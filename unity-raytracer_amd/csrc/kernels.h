@@ -17,6 +17,10 @@ constexpr bool kWaveClockBuild = true;
 constexpr bool kWaveClockBuild = false;
 #endif
 
+// Frames (row shards) of at most this many tiles launch render_kernel's
+// 5-wave instances (trace.hip), the only ones with the one-sample split path.
+constexpr int kShardTilesMax = 70000;
+
 // One frame (or one row shard of it): CastPixelRays + Shade, RayTracingSetup.cs:275-366.
 // Megakernel: one lane per sample, whole Whitted chain in one launch (trace.hip).
 // Longest-first tile order for the next frame (trace.hip).

@@ -259,6 +259,12 @@ struct FrameDev {
     float cut_ax[3], cut_bx[3], cut_ay[3], cut_by[3];
     float cut_a[3], cut_r[3], cut_u[3];  // A, R, U (the central ray's direction orders the entries)
     uint4 *wave_clock;  // measuring builds only (RT_WAVE_CLOCK): per-wave {start lo, start hi, duration, tile}
+    // finely split tiles: 64 >> s16_shift waves each (2: a pixel per wave; 0: a
+    // sample per wave, whose pixel sums meet here — per split tile its 64
+    // samples as float4 and its 16 pixels' arrival counts)
+    int s16_shift;
+    float *split_samples;
+    int *split_count;
 };
 
 }  // namespace rtd

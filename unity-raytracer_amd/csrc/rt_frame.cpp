@@ -147,6 +147,7 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.tile_h = th;
     F.tiles_x = (F.res_x + tw - 1) / tw;
     F.tiles_x_magic = F.tiles_x <= 1 ? 0xffffffffu : (unsigned)((1ull << 32) / (unsigned long long)F.tiles_x);
+    F.s16_shift = 2;  // finely split tiles: a pixel per wave (lpt_prepare may choose a sample per wave)
     const int tiles_y = (F.local_rows + th - 1) / th;
     F.num_tiles = F.res_x > 0 ? F.tiles_x * tiles_y : 0;
     const bool f8 = (prm->flags & RT_FLAG_OUT_RGBA8) != 0, f16 = (prm->flags & RT_FLAG_OUT_RGBA16F) != 0,
@@ -239,6 +240,11 @@ constexpr int kSplit16MaxTiles = RT_EXP_SPLIT16MAX;  // measuring builds only
 constexpr int kSplit16MaxTiles = 70000;
 #endif
 constexpr int kSplit16DivLarge = 4096;
+#ifdef RT_EXP_S64LONE
+constexpr bool kSample16Lone = RT_EXP_S64LONE != 0;  // measuring builds only
+#else
+constexpr bool kSample16Lone = true;  // lone shards of 24,000-70,000 tiles: a sample per wave too
+#endif
 // ... and a shard of that size with no other frame beside it (lpt_prepare
 // overlapped_frame: a synchronous Update() frame of one rank) its slowest
 // 1/1024: a 1/2 C3 shard's single frame -10.6 %, frames in flight +-0 (r04n;
@@ -444,6 +450,25 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         ls->hints_scene = ctx->scene_version;
         ls->hints_key = key;
         F.shadow_hint = (int *)ls->hints.p;
+    }
+    // In small shards the finely split tiles go one step further, to a sample
+    // per wave (F.s16_shift 0; the shard instance sums each pixel's four
+    // samples when the last arrives): a pixel's four samples no longer wait for
+    // each other's divergent mirror chains.  1/8 C3 shard single frame -18 %,
+    // frames in flight -4 %; a 1/4 shard -9 % single but +7 % in flight, so
+    // only lone frames there; whole frames +6 % (r04r, one0..one3 / s64).
+    if (F.split16_tiles > 0 && !count && !levels && F.spp == 4 && F.num_tiles <= rtk::kShardTilesMax &&
+        (F.num_tiles <= kSplitMaxTiles || (kSample16Lone && !overlapped_frame(ctx, prm)))) {
+        F.s16_shift = 0;
+        const size_t sb = (size_t)F.split16_tiles * rtd::kWaveSize * 4 * sizeof(float);
+        const size_t cb = (size_t)F.split16_tiles * (rtd::kWaveSize / 4) * sizeof(int);
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->split_samples, sb));
+        if (cb > ls->split_count.cap) {  // counts start at 0; the fourth arrival resets its pixel's
+            HIP_OR_FAIL(ctx, ensure(ctx, ls->split_count, cb));
+            HIP_OR_FAIL(ctx, hipMemsetAsync(ls->split_count.p, 0, ls->split_count.cap, ctx->stream));
+        }
+        F.split_samples = (float *)ls->split_samples.p;
+        F.split_count = (int *)ls->split_count.p;
     }
     if (levels && !(F.max_bounces > rtd::kMaxBounces)) {
         // the levels kernel dispatches XCD-aware stripes in row order

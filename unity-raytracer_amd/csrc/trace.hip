@@ -291,7 +291,12 @@ constexpr int kMkMinWavesShard = 5;
 // LDS stack entries of the 5-wave instances: 24 (a 1/2 C3 shard, single frame:
 // 0.199 ms with 16 entries, 0.186 with 24, r04i; the LDS does not bind at five waves)
 constexpr int kStackShard = 24;
-constexpr int kShardTiles = 70000;  // rt_frame.cpp kSplit16MaxTiles: a 1/2 shard of 1080p at 4 spp
+// Waves of one finely split tile: 64 >> F.s16_shift — 16 waves of one
+// pixel's four samples (shift 2), or in small shards 64 waves of one sample
+// (shift 0, rt_frame.cpp lpt_prepare): a pixel's four samples then meet in
+// F.split_samples and the last to arrive sums them (render_tile).
+__device__ __forceinline__ int s16_shift(const FrameDev &F) { return __builtin_amdgcn_readfirstlane(F.s16_shift); }
+constexpr int kShardTiles = rtk::kShardTilesMax;  // a 1/2 shard of 1080p at 4 spp
 // Waves per megakernel workgroup.  A workgroup's slot is recycled only when
 // all of its waves are done, and path lengths vary a lot between tiles, so
 // small workgroups keep the CUs fuller near the end of each wave "round".
@@ -308,13 +313,20 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 template <bool COUNT, bool DEEP, bool Q4, bool HINT, bool MOOT>
 __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
                                             int *wstack, int tile, int part, int pshift, int lane, Counts &cnt,
-                                            SegClock &sg) {
+                                            SegClock &sg, int sidx) {
+    (void)sidx;
     // the cut entries do not depend on the tile: their loads are issued first
     rtp::CutLane cl;
     if (!COUNT) cl = rtp::cut_load(S);
     int px, ly, gy, s;
+#ifdef RT_EXP_ONESAMPLE
+    // measuring builds only (wrong images): a sixteenth-wave traces its pixel's first sample alone
+    const bool active = rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) &&
+                        (part < 0 || ((lane >> pshift) == part && (pshift != 2 || (lane & 3) == RT_EXP_ONESAMPLE)));
+#else
     const bool active =
         rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
+#endif
     f3 color = mk(0.0f, 0.0f, 0.0f);
     // a wave whose samples all surely miss the padded Scene.AABB is background
     // without its exact rays (shade.h sky_maybe; the counting launch traces all)
@@ -350,6 +362,33 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     const int lane2 = rtt::lane_id();
     const bool active2 =
         rts::slot_pixel<Q4>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
+    if (HINT && !COUNT && pshift == 0 && (Q4 || F.spp == 4)) {
+        // a one-sample wave of a split pixel: its sample goes to the pixel's
+        // slots by write-through (sc1) stores, then the pixel's arrival count;
+        // the fourth arrival sums the samples in sample order, as sample_sum
+        if (active2) {
+            typedef __attribute__((address_space(1))) unsigned gu32;
+            typedef __attribute__((address_space(1))) int gi32;
+            float *sp = F.split_samples + ((size_t)sidx * kWaveSize + lane2) * 4;
+            __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
+            int *cp = F.split_count + sidx * (kWaveSize / 4) + (lane2 >> 2);
+            if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
+                const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (lane2 & ~3)) * 4;
+                auto ld = [](const float *q) {
+                    return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                };
+                f3 v = mk(ld(b), ld(b + 1), ld(b + 2));
+                for (int k = 1; k < 4; ++k) v = v + mk(ld(b + 4 * k), ld(b + 4 * k + 1), ld(b + 4 * k + 2));
+                v = v * 0.25f;
+                rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+                __hip_atomic_store((gi32 *)cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
+            }
+        }
+        return sky;
+    }
     if (active2 && s == 0) {
         f3 v = sum;
         if (Q4)
@@ -383,7 +422,8 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     const int wid = blockIdx.x * kMkWaves + wave;
     const int split16 = SPLIT ? F.split16_tiles : 0;
     const int split = SPLIT ? F.split_tiles : 0;
-    if (wid >= F.num_tiles + 15 * split16 + 3 * split) return;  // wave-uniform
+    const int s16sh = SPLIT ? s16_shift(F) : 2;  // one finely split tile: 64 >> s16sh waves
+    if (wid >= F.num_tiles + ((64 >> s16sh) - 1) * split16 + 3 * split) return;  // wave-uniform
 #ifdef RT_WAVE_CLOCK
     const unsigned long long rc0 = __builtin_amdgcn_s_memrealtime();  // constant 100 MHz clock
 #endif
@@ -393,16 +433,16 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     // quarter-waves each (16 lanes: a smaller, more coherent packet, a
     // shorter wave)
     int idx, part = -1, pshift = 4;
-    if (SPLIT && wid < 16 * split16) {
-        idx = wid >> 4;
-        part = wid & 15;
-        pshift = 2;
-    } else if (SPLIT && wid < 16 * split16 + 4 * split) {
-        const int w1 = wid - 16 * split16;
+    if (SPLIT && wid < (split16 << (6 - s16sh))) {
+        idx = wid >> (6 - s16sh);
+        part = wid & ((64 >> s16sh) - 1);
+        pshift = s16sh;
+    } else if (SPLIT && wid < (split16 << (6 - s16sh)) + 4 * split) {
+        const int w1 = wid - (split16 << (6 - s16sh));
         idx = split16 + (w1 >> 2);
         part = w1 & 3;
     } else {
-        idx = wid - 15 * split16 - 3 * split;
+        idx = wid - ((64 >> s16sh) - 1) * split16 - 3 * split;
     }
     // the tile index is wave-uniform and kept in an SGPR: the slot -> pixel
     // integer math runs on the scalar unit and nothing of it is spilled
@@ -418,7 +458,8 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     // the shadow occluder hints (packet.h HINT) pay off in small frames only:
     // the 5-wave split instance (row shards), not the whole-frame one
     constexpr bool HINT = SPLIT && W < 6;
-    const bool sky = render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg);
+    const bool sky =
+        render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, idx);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
@@ -790,7 +831,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     FrameDev F = F0;
     F.primary_total = active_samples(F.res_x, F.res_y, F.local_rows, F.row0, F.band_index, F.band_count, F.band_rows,
                                      F.spp);
-    int blocks = (F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles + kMkWaves - 1) / kMkWaves;
+    int blocks = (render_mega_waves(F) + kMkWaves - 1) / kMkWaves;
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     const bool shard = F.num_tiles <= kShardTiles;  // a small frame: its slowest waves set its time
     constexpr int W5 = kMkMinWavesShard;
@@ -835,7 +876,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
 }
 
 int render_mega_waves(const FrameDev &F) {
-    return F.num_tiles <= 0 ? 0 : F.num_tiles + 15 * F.split16_tiles + 3 * F.split_tiles;
+    return F.num_tiles <= 0 ? 0 : F.num_tiles + ((64 >> F.s16_shift) - 1) * F.split16_tiles + 3 * F.split_tiles;
 }
 
 // Longest-first dispatch for the next frame: tiles sorted by the cost key this
