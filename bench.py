@@ -416,7 +416,8 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    ctx.set_scene(fr.scene)
+    ctx.set_scene(fr.scene)  # rt_set_scene's default: the 4-wide device LBVH (host SAH if too deep)
+    bvh_build = {0: "host SAH, 4-wide", 1: "device LBVH, 4-wide"}.get(ctx.scene_info()["build"], "other")
     rx, ry = fr.plane.ResolutionX, fr.plane.ResolutionY
     R = 8
     band_count = world if not args.sim_bands else args.sim_bands
@@ -699,6 +700,7 @@ def main():
                 "spp": fr.spp,
                 "depth": fr.max_bounces,
                 "triangles": fr.scene.triangle_count,
+                "bvh_build": bvh_build,
                 "parallelism": f"row-bands x{world}" + ((" + gloo gather (rehearsal)" if gloo else " + RCCL gather")
                                                         if dist_on else ""),
                 "rays_per_frame": rays_per_frame,

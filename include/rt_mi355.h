@@ -268,15 +268,17 @@ const char *rt_last_error(const rt_ctx *ctx);
 int rt_set_stream(rt_ctx *ctx, void *hip_stream);
 
 /* Upload a scene: copies every array to HBM, computes Scene.AABB exactly as
- * Scene.CalculateAABB (Scene.cs:17-41) and builds the BVH.  Replaces
- * RayTracingSetup.UpdateScene()'s result (:120-128). */
+ * Scene.CalculateAABB (Scene.cs:17-41) and builds the BVH — on the device
+ * (RT_BUILD_LBVH_GPU; the host SAH when that tree would be too deep for the
+ * traversal stack).  Replaces RayTracingSetup.UpdateScene()'s result
+ * (:120-128).  rt_set_scene_ex chooses the builder. */
 int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *scene);
 
 /* BVH builders for rt_set_scene_ex. */
-#define RT_BUILD_SAH_HOST 0   /* binned SAH on the host, collapsed to 4-wide nodes (fastest traversal) */
+#define RT_BUILD_SAH_HOST 0   /* binned SAH on the host, collapsed to 4-wide nodes */
 #define RT_BUILD_LBVH_GPU 1   /* linear BVH built on the GPU (Morton + radix sort + Karras), collapsed
-                                 to 4-wide nodes on the GPU: for per-frame scene rebuilds
-                                 (RayTracingSetup.cs:120-128) */
+                                 to 4-wide nodes on the GPU (rt_set_scene's default; also for
+                                 per-frame scene rebuilds, RayTracingSetup.cs:120-128) */
 #define RT_BUILD_LBVH_GPU_BVH2 2  /* the same tree left 2-wide (comparison / diagnostics) */
 #define RT_BUILD_SAH_REFIT 3  /* rt_set_scene_source_ex only: the host SAH tree once, then every
                                  rt_update_mesh_transforms refits it on the device (same topology and

@@ -24,6 +24,21 @@ def _same(a, b):
     return np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
+def test_default_build_is_the_device_lbvh(gpu_ctx, rt):
+    """rt_set_scene (no builder named) builds the 4-wide device LBVH; the frame
+    equals the host SAH tree's bit for bit."""
+    fr = rt.make("C2").with_resolution(160, 90)
+    gpu_ctx.set_scene(fr.scene)
+    info = gpu_ctx.scene_info()
+    assert info["build"] == LBVH and info["bvh_width"] == 4
+    a, sa = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+    gpu_ctx.set_scene(fr.scene, 0)
+    b, sb = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+    assert _same(a, b)
+    assert (sa.primary_rays, sa.shadow_rays, sa.reflection_rays) == (sb.primary_rays, sb.shadow_rays,
+                                                                     sb.reflection_rays)
+
+
 def test_scene_info(gpu_ctx, rt):
     fr = rt.make("C3")
     gpu_ctx.set_scene(fr.scene, 0)

@@ -44,10 +44,13 @@ def main():
     streams = [torch.cuda.Stream() for _ in range(4)]
     V = []
     for v in names:
-        path = None if v == "default" else os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", v,
-                                                         "librt_mi355.so")
+        # "name@lbvh" / "name@sah": the same library with the scene built by the named builder
+        # (no suffix: rt_set_scene's default)
+        lib, _, build = v.partition("@")
+        path = None if lib == "default" else os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", lib,
+                                                           "librt_mi355.so")
         ctx = rt.Context(lib_path=path)
-        ctx.set_scene(fr.scene)
+        ctx.set_scene(fr.scene, build={"lbvh": rt.abi.RT_BUILD_LBVH_GPU, "sah": rt.abi.RT_BUILD_SAH_HOST}.get(build))
         outs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in streams]
         V.append({"name": v, "ctx": ctx, "outs": outs, "single": [], "stream": []})
     cam, pl = rt.raytracing.camera_struct(fr.camera), rt.raytracing.plane_struct(fr.plane)

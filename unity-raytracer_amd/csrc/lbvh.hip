@@ -13,6 +13,11 @@ using rtm::mk;
 
 constexpr int kThreads = 256;
 constexpr int kLbvhLeaf = 4;  // max primitives per collapsed leaf (2-bit count field)
+#ifdef RT_EXP_LBVH_NODECOST
+constexpr float kLeafNodeCost = RT_EXP_LBVH_NODECOST;  // measuring builds only
+#else
+constexpr float kLeafNodeCost = 1.0f;  // a node step against one primitive test (k_small's leaf rule)
+#endif
 
 inline int blocks_for(int n) { return (n + kThreads - 1) / kThreads; }
 
@@ -357,7 +362,8 @@ __global__ void k_small(int n, const int2 *range, const int *gate_pos, const rtd
         }
         const int c0 = nd.d.x >= 0 ? range[nd.d.x].y - range[nd.d.x].x + 1 : 1;
         const float ap = fmaxf(half_area(lp, hp), 1e-30f);
-        const float split = 1.0f + (half_area(l0, h0) * (float)c0 + half_area(l1, h1) * (float)(cnt - c0)) / ap;
+        const float split =
+            kLeafNodeCost + (half_area(l0, h0) * (float)c0 + half_area(l1, h1) * (float)(cnt - c0)) / ap;
         ok = (float)cnt <= split;
     }
     small[i] = ok ? 1 : 0;

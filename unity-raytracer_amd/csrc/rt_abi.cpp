@@ -74,7 +74,16 @@ int rt_set_stream(rt_ctx *ctx, void *hip_stream) {
     return RT_OK;
 }
 
-int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) { return rt_set_scene_ex(ctx, sc, RT_BUILD_SAH_HOST); }
+// The default builder is the device LBVH collapsed to 4-wide nodes: a
+// millisecond build instead of tens (host SAH) and, measured at round 4's final
+// kernels, the faster tree to trace too (C5 -7 %, C4 -3 %, C3 -1..-3 %, C2 +-0;
+// profiles/r04/abx_r04w).  A scene whose LBVH is too deep for the traversal
+// stack (or that the LBVH path rejects) is built by the host SAH instead.
+int rt_set_scene(rt_ctx *ctx, const rt_scene_desc *sc) {
+    const int st = rt_set_scene_ex(ctx, sc, RT_BUILD_LBVH_GPU);
+    if (st != RT_E_SCENE || !ctx) return st;
+    return rt_set_scene_ex(ctx, sc, RT_BUILD_SAH_HOST);
+}
 
 int rt_set_scene_ex(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build) {
     if (!ctx) return RT_E_INVALID;

@@ -56,7 +56,14 @@ constexpr int kLvWavesHighSpp = 8;
 // fits 32 waves per CU) stashes 15 floats — all but the view vector: C5 HBM
 // writes 19.6 -> 10.6 GB and reads 9.2 -> 3.4 GB per launch at the same time
 // (r04n; 9 floats +1.3 %, 15 at 7 waves +2.4 %, 18 at 7 waves +6 %).
-constexpr int kXcdStripeRows = 4;  // tile rows per XCD stripe (render_levels_kernel dispatch)
+// Tile rows per XCD stripe (render_levels_kernel dispatch), per instance:
+// <= 16 spp (2x2-pixel tiles) 1, 64 spp (one-pixel tiles) 4 — C4 -1.6 % with
+// 1 against 4, C5 +0.5 % (2: +-0, 16: +2.6 %; r04ad).
+#ifdef RT_EXP_XCDROWS
+constexpr int kXcdStripeRowsLow = RT_EXP_XCDROWS, kXcdStripeRowsHigh = RT_EXP_XCDROWS;  // measuring builds
+#else
+constexpr int kXcdStripeRowsLow = 1, kXcdStripeRowsHigh = 4;
+#endif
 
 #ifdef RT_EXP_LVSTASH_HI
 constexpr int kLvStashHigh = RT_EXP_LVSTASH_HI;  // measuring builds only (0, 9, 15 or 18)
@@ -84,11 +91,11 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     // XCD-aware dispatch (blocks b and b + 8 share an XCD, MI355X_MICROARCH.md
     // "Workgroup dispatch"; placement is a speed matter only): XCD group x
-    // renders the stripes x, x + 8, ... of kXcdStripeRows tile rows in row
+    // renders the stripes x, x + 8, ... of kXcdStripeRows* tile rows in row
     // order, so each XCD's L2 serves the geometry of one eighth of the screen
     // instead of all of it — C5 -3 %, C4 -2 % with frames in flight (r04g).
     // A frame's tiles are all here exactly once, whatever the placement.
-    const int zs = kXcdStripeRows * F.tiles_x;
+    const int zs = (MIN_WAVES == kLvWavesLowSpp ? kXcdStripeRowsLow : kXcdStripeRowsHigh) * F.tiles_x;
     const int k = blockIdx.x >> 3;
     const int wid = ((k / zs) * 8 + (blockIdx.x & 7)) * zs + k % zs;  // the tile itself
     if (wid >= F.num_tiles) return;  // wave-uniform (the last stripes' padding)
@@ -276,7 +283,8 @@ namespace rtk {
 hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F, hipStream_t stream) {
     if (F.num_tiles <= 0) return hipSuccess;
     // whole groups of eight stripes (render_levels_kernel's XCD-aware dispatch)
-    const long long zs = (long long)kXcdStripeRows * F.tiles_x, ns = (F.num_tiles + zs - 1) / zs;
+    const long long rows = F.spp <= 16 ? kXcdStripeRowsLow : kXcdStripeRowsHigh;  // the instance launched below
+    const long long zs = rows * F.tiles_x, ns = (F.num_tiles + zs - 1) / zs;
     const long long grid = 8 * ((ns + 7) / 8) * zs;
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
     if (F.spp <= 16)

@@ -116,11 +116,15 @@ class Context:
     def set_stream(self, stream_handle: int):
         self._check(self.lib.rt_set_stream(self.h, C.c_void_p(stream_handle)))
 
-    def set_scene(self, scene: Scene, build: int = abi.RT_BUILD_SAH_HOST):
-        """Upload a scene and build its BVH: host SAH (4-wide) or on-device
-        LBVH (2-wide, for per-frame rebuilds).  Renders are identical."""
+    def set_scene(self, scene: Scene, build: Optional[int] = None):
+        """Upload a scene and build its BVH: None = rt_set_scene's default (the
+        on-device LBVH, 4-wide; the host SAH if that tree is too deep), or an
+        explicit RT_BUILD_* through rt_set_scene_ex.  Renders are identical."""
         desc = scene.to_desc()
-        self._check(self.lib.rt_set_scene_ex(self.h, desc.ref(), int(build)))
+        if build is None:
+            self._check(self.lib.rt_set_scene(self.h, desc.ref()))
+        else:
+            self._check(self.lib.rt_set_scene_ex(self.h, desc.ref(), int(build)))
         self._scene_desc = desc  # keep arrays alive for the duration of the call only; harmless
 
     def set_scene_source(self, base: Scene, sources, build: Optional[int] = None):
