@@ -326,9 +326,10 @@ def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
 def test_split_sixteenths_of_large_shards_is_invisible(gpu_ctx, rt):
     """Shards of 24,000-70,000 tiles (a 1/2 and a 1/4 shard of 1080p C3) run
     their slowest tiles finely split — synchronous (lone) frames their slowest
-    1/1024 as one-sample waves — and a whole synchronous 1080p frame its
-    slowest 1/4096 as one-pixel waves (the 6-wave split instance): same bits
-    and ray counts as row-major frames."""
+    1/1024, the 1/4 shard (<= 40,000 tiles) as one-sample waves, the 1/2 shard
+    as one-pixel waves — and a whole synchronous 1080p frame its slowest
+    1/4096 as one-pixel waves (the 6-wave split instance): same bits and ray
+    counts as row-major frames."""
     fr = rt.make("C3")
     gpu_ctx.set_scene(fr.scene)
     for kw in (dict(band_index=0, band_count=2, band_rows=8), dict(band_index=3, band_count=4, band_rows=8), {}):

@@ -241,9 +241,9 @@ constexpr int kSplit16MaxTiles = 70000;
 #endif
 constexpr int kSplit16DivLarge = 4096;
 #ifdef RT_EXP_S64LONE
-constexpr bool kSample16Lone = RT_EXP_S64LONE != 0;  // measuring builds only
+constexpr int kSample16LoneTiles = RT_EXP_S64LONE;  // measuring builds only
 #else
-constexpr bool kSample16Lone = true;  // lone shards of 24,000-70,000 tiles: a sample per wave too
+constexpr int kSample16LoneTiles = 40000;  // lone shards up to this many tiles: a sample per wave too
 #endif
 // ... and a shard of that size with no other frame beside it (lpt_prepare
 // overlapped_frame: a synchronous Update() frame of one rank) its slowest
@@ -454,11 +454,12 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // In small shards the finely split tiles go one step further, to a sample
     // per wave (F.s16_shift 0; the shard instance sums each pixel's four
     // samples when the last arrives): a pixel's four samples no longer wait for
-    // each other's divergent mirror chains.  1/8 C3 shard single frame -18 %,
-    // frames in flight -4 %; a 1/4 shard -9 % single but +7 % in flight, so
-    // only lone frames there; whole frames +6 % (r04r, one0..one3 / s64).
+    // each other's divergent mirror chains.  1/8 C3 shard single frame -20 %,
+    // frames in flight -13 %; a 1/4 shard -15 % single but worse in flight, so
+    // only lone frames there; a lone 1/2 shard +5 %, whole frames +6 %
+    // (r04r, r04ag).
     if (F.split16_tiles > 0 && !count && !levels && F.spp == 4 && F.num_tiles <= rtk::kShardTilesMax &&
-        (F.num_tiles <= kSplitMaxTiles || (kSample16Lone && !overlapped_frame(ctx, prm)))) {
+        (F.num_tiles <= kSplitMaxTiles || (F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm)))) {
         F.s16_shift = 0;
         const size_t sb = (size_t)F.split16_tiles * rtd::kWaveSize * 4 * sizeof(float);
         const size_t cb = (size_t)F.split16_tiles * (rtd::kWaveSize / 4) * sizeof(int);

@@ -217,25 +217,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
     // lane ids recomputed (rtt::lane_id), not kept live across the levels
     const int lane2 = rtt::lane_id();
-#ifdef RT_EXP_LDSSUM
-    // measuring builds: the pixel sums through the (now free) LDS stash — each
-    // lane's sample written once, each pixel's sample-0 lane reads its
-    // pixel's samples in order (no per-sample lane permutations)
-    f3 sum = term;
-    if (STASH >= 3 && F.spp >= 16) {
-        volatile float *vs = stash_mem;
-        vs[lane2] = term.x;
-        vs[kWaveSize + lane2] = term.y;
-        vs[2 * kWaveSize + lane2] = term.z;
-        if ((lane2 & (F.spp - 1)) == 0)
-            for (int k = 1; k < F.spp; ++k)
-                sum = sum + mk(vs[lane2 + k], vs[kWaveSize + lane2 + k], vs[2 * kWaveSize + lane2 + k]);
-    } else {
-        sum = rts::sample_sum(term, lane2, F.spp);
-    }
-#else
     const f3 sum = rts::sample_sum(term, lane2, F.spp);
-#endif
     {
         int tile2 = __builtin_amdgcn_readfirstlane(tile);
         asm volatile("" : "+s"(tile2));
