@@ -308,10 +308,11 @@ def test_longest_first_order_is_invisible(gpu_ctx, rt):
 
 def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
     """Small frames (<= 24,000 tiles) run their slowest tiles, as measured by
-    the previous re-sort, as four quarter-waves (the slowest 1/2048 as 64
-    one-sample waves at 4 spp, whose pixel sums meet through write-through
-    stores and an arrival count): same bits and same ray counts as row-major
-    whole-tile frames, for a whole frame and for a row shard."""
+    the previous re-sort, as four quarter-waves (the slowest 1/2048 — in
+    synchronous frames as 64 one-sample waves at 4 spp, whose pixel sums meet
+    through write-through stores and an arrival count): same bits and same ray
+    counts as row-major whole-tile frames, for a whole frame and for a row
+    shard."""
     fr = rt.make("C3").with_resolution(640, 360)
     gpu_ctx.set_scene(fr.scene)
     for kw in ({}, dict(band_index=1, band_count=3, band_rows=8)):

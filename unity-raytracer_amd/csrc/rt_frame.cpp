@@ -243,7 +243,7 @@ constexpr int kSplit16DivLarge = 4096;
 #ifdef RT_EXP_S64LONE
 constexpr int kSample16LoneTiles = RT_EXP_S64LONE;  // measuring builds only
 #else
-constexpr int kSample16LoneTiles = 40000;  // lone shards up to this many tiles: a sample per wave too
+constexpr int kSample16LoneTiles = 40000;  // lone shards up to this many tiles: a sample per wave
 #endif
 // ... and a shard of that size with no other frame beside it (lpt_prepare
 // overlapped_frame: a synchronous Update() frame of one rank) its slowest
@@ -454,12 +454,13 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // In small shards the finely split tiles go one step further, to a sample
     // per wave (F.s16_shift 0; the shard instance sums each pixel's four
     // samples when the last arrives): a pixel's four samples no longer wait for
-    // each other's divergent mirror chains.  1/8 C3 shard single frame -20 %,
-    // frames in flight -13 %; a 1/4 shard -15 % single but worse in flight, so
-    // only lone frames there; a lone 1/2 shard +5 %, whole frames +6 %
-    // (r04r, r04ag).
+    // each other's divergent mirror chains.  Lone frames only (nothing beside
+    // them hides their slowest chain): a 1/8 C3 shard's single frame -20 %, a
+    // 1/4 shard's -15 %; a lone 1/2 shard +5 %, whole frames +6 %; with four
+    // frames in flight a 1/8 shard's throughput is -3 % to +-0 (r04r, r04ag,
+    // r04ai, 200-frame runs alternated on one box).
     if (F.split16_tiles > 0 && !count && !levels && F.spp == 4 && F.num_tiles <= rtk::kShardTilesMax &&
-        (F.num_tiles <= kSplitMaxTiles || (F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm)))) {
+        F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm)) {
         F.s16_shift = 0;
         const size_t sb = (size_t)F.split16_tiles * rtd::kWaveSize * 4 * sizeof(float);
         const size_t cb = (size_t)F.split16_tiles * (rtd::kWaveSize / 4) * sizeof(int);
