@@ -458,9 +458,12 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // them hides their slowest chain): a 1/8 C3 shard's single frame -20 %, a
     // 1/4 shard's -15 %; a lone 1/2 shard +5 %, whole frames +6 %; with four
     // frames in flight a 1/8 shard's throughput is -3 % to +-0 (r04r, r04ag,
-    // r04ai, 200-frame runs alternated on one box).
+    // r04ai, 200-frame runs alternated on one box).  Not in the bands of a
+    // multi-device frame (rt_group.cpp): its members' frames run side by side,
+    // and two full GPU-suite runs of 8-member groups on one device stalled
+    // with them (r04s, r04an; cause not found, 5 other runs passed).
     if (F.split16_tiles > 0 && !count && !levels && F.spp == 4 && F.num_tiles <= rtk::kShardTilesMax &&
-        F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm)) {
+        F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm) && !ctx->in_group_frame) {
         F.s16_shift = 0;
         const size_t sb = (size_t)F.split16_tiles * rtd::kWaveSize * 4 * sizeof(float);
         const size_t cb = (size_t)F.split16_tiles * (rtd::kWaveSize / 4) * sizeof(int);

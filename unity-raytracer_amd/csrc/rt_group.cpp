@@ -368,7 +368,9 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
             // frame of this root stream has been reassembled
             HIP_OR_FAIL(ctx, hipStreamWaitEvent(m->stream, gs->gather_free, 0));
         }
+        m->in_group_frame = true;
         st = run_frame(m, F[(size_t)i], &mp[(size_t)i], out, nullptr, t0, nullptr, 0);
+        m->in_group_frame = false;
         if (st) {
             if (i) ctx->err = m->err;
             return st;

@@ -337,6 +337,7 @@ struct rt_ctx {
     int debug_fail_slab = -1;  // rt_debug_set(RT_DEBUG_FAIL_SLAB): rt_render fails before this row slab
     // rt_debug_set(RT_DEBUG_WAVE_CLOCKS), measuring builds: the last render_kernel launch's per-wave clocks
     bool debug_wave_clock = false;
+    bool in_group_frame = false;  // rendering one band of a multi-device frame (rt_group.cpp group_frame)
     rti::GrowBuf wave_clock;
     int64_t wave_clock_bytes = 0;
 };
