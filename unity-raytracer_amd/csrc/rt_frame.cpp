@@ -242,8 +242,13 @@ constexpr int kSplit16MaxTiles = 70000;
 constexpr int kSplit16DivLarge = 4096;
 // A lone whole frame (more than kSplit16MaxTiles tiles, no other frame beside
 // it) splits only its slowest 1/16384: C3 single frame -1.7 %, C2 -2.1 %
-// against 1/4096 (1/8192: -1.1 / -1.1 %; r04aq, r04ar).
+// against 1/4096 (1/8192: -1.1 / -1.1 %; r04aq, r04ar); 1/32768 +6 %, one
+// tile +15 % on C3 (r04au).
+#ifdef RT_EXP_SPLIT16WHOLE
+constexpr int kSplit16DivWhole = RT_EXP_SPLIT16WHOLE;  // measuring builds only
+#else
 constexpr int kSplit16DivWhole = 16384;
+#endif
 #ifdef RT_EXP_S64LONE
 constexpr int kSample16LoneTiles = RT_EXP_S64LONE;  // measuring builds only
 #else
