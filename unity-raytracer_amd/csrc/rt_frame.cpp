@@ -223,7 +223,11 @@ int prepare_wavefront(rt_ctx *ctx, const rtd::FrameDev &F, int &chunk_tiles, rtw
 // slowest of them (1/2048 of the tiles) go further, to sixteen waves of one
 // pixel each: a 1/8 shard's single frame -14 % more, throughput with frames
 // in flight +-1 % (1/512 or more: -5..-15 %).
+#ifdef RT_EXP_SPLIT16DIV
+constexpr int kSplit16Div = RT_EXP_SPLIT16DIV;  // measuring builds only
+#else
 constexpr int kSplit16Div = 2048;  // of those, 1/kSplit16Div of the tiles as sixteenth-waves; 0: off
+#endif
 constexpr int kSplitDiv = 256;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
 // Larger shards (up to 70,000 tiles: a 1/2 or 1/4 shard of 1080p) split only
 // their slowest 1/4096 into sixteenth-waves: single frame -15..-30 %,
