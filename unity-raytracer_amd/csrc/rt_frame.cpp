@@ -441,7 +441,11 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
         // sixteenth-waves (4 lanes) must hold whole pixels too
         if (kSplit16Div > 0 && 4 % F.spp == 0) {
-            F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / kSplit16Div));
+            // a lone shard's (one-sample waves, below) twice as many: a 1/8
+            // C3 share's single frame -11.9 %; in flight +2.6 % (r04av)
+            const bool sample_waves = F.spp == 4 && !overlapped_frame(ctx, prm) && !ctx->in_group_frame;
+            const int div = sample_waves ? kSplit16Div / 2 : kSplit16Div;
+            F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / div));
             F.split_tiles -= F.split16_tiles;
         }
     } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
