@@ -429,6 +429,18 @@ float rt_spec_threshold(void);
  * measuring build is compiled with -DRT_WAVE_CLOCK.  One
  * frame in flight at a time: every launch overwrites the records. */
 #define RT_DEBUG_WAVE_CLOCKS 2
+/* Testing only: RT_DEBUG_GROUP_SAMPLE_WAVES (value 1: on) lets the bands of
+ * this multi-device context's frames run their slowest pixels as one-sample
+ * waves, which its frames otherwise never do (rt_frame.cpp lpt_prepare); the
+ * stall probe (tools/stall_probe.py) uses it to exercise that configuration. */
+#define RT_DEBUG_GROUP_SAMPLE_WAVES 3
+/* Diagnostics: rt_debug_read(ctx, RT_DEBUG_HOST_WAITS, out, cap, &n) writes
+ * a text report (NUL-terminated, truncated to cap) of every host thread that
+ * is inside one of the library's blocking runtime calls right now (the call,
+ * its device and for how long) and, for a non-NULL ctx, whether each stream of
+ * the context and its members still has work pending.  Safe to call from
+ * another thread while a call of the context is blocked; ctx may be NULL. */
+#define RT_DEBUG_HOST_WAITS 4
 int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value);
 int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, int64_t *bytes_written);
 

@@ -1,5 +1,7 @@
+import faulthandler
 import os
 import sys
+import threading
 
 import pytest
 
@@ -17,6 +19,48 @@ import _rt_pkg  # noqa: E402
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device")
+
+
+# Per-test stall watchdog (GPU tests): a test that runs longer than this is
+# taken to be stalled — every host thread's Python stack, the library's
+# report of the blocking calls its threads sit in (rt_debug_read
+# RT_DEBUG_HOST_WAITS) and each open context's stream states go to stderr,
+# and the process exits (status 70), well before the GPU box's 3-minute
+# silence limit would kill the run without a word.  The whole GPU suite takes
+# about a minute; no single test takes more than a few seconds.
+WATCHDOG_S = float(os.environ.get("RT_TEST_WATCHDOG_S", "100"))
+
+
+def _stall_dump(name):
+    err = sys.__stderr__
+    try:
+        err.write(f"\n=== watchdog: {name} still running after {WATCHDOG_S:.0f} s ===\n")
+        err.flush()
+        rtmod = sys.modules.get("unity_raytracer_amd.raytracing") or _rt_pkg.load().raytracing
+        ctxs = [c for c in list(rtmod.LIVE_CONTEXTS) if getattr(c, "h", None)]
+        err.write(rtmod.host_waits_report(None) + "\n")
+        for c in ctxs:
+            err.write(rtmod.host_waits_report(c) + "\n")
+        err.flush()
+    except Exception as e:  # the dump must not hide the stall itself
+        err.write(f"(library report failed: {e!r})\n")
+    faulthandler.dump_traceback(file=err, all_threads=True)
+    err.flush()
+    os._exit(70)
+
+
+@pytest.fixture(autouse=True)
+def _watchdog(request):
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    t = threading.Timer(WATCHDOG_S, _stall_dump, args=(request.node.nodeid,))
+    t.daemon = True
+    t.start()
+    try:
+        yield
+    finally:
+        t.cancel()
 
 
 @pytest.fixture(scope="session")

@@ -50,3 +50,24 @@ def test_spec_pow_matches_host_pow(st):
     both_nan = np.isnan(got) & np.isnan(want)
     bad = np.flatnonzero(diff & ~both_nan)
     assert bad.size == 0, f"{bad.size} mismatches, e.g. x={x[bad[0]]!r} y={y[bad[0]]!r}: {got[bad[0]]!r} vs {want[bad[0]]!r}"
+
+
+@pytest.mark.parametrize("lds_entries", [16, 24])
+@pytest.mark.parametrize("depth", [1, 5, 8, 9, 30, 42])
+def test_lane_stack_reaches_the_accepted_depth(st, depth, lds_entries):
+    """The per-lane stack (LDS part + private overflow) of both render_kernel
+    shapes holds 3 x depth pending entries — the most a tree the builders
+    accept (3 x (depth + 1) <= kStackTotal) can push — and returns them in
+    order: every leaf of the comb is tested once and the stack-bottom leaf,
+    popped last, is the closest hit (the 24-entry instances once
+    lost their LDS depth in traverse())."""
+    st.rt_selftest_deep_stack.argtypes = [C.c_int, C.c_int, C.c_void_p]
+    st.rt_selftest_deep_stack.restype = C.c_int
+    out = np.zeros(4, np.int32)
+    assert st.rt_selftest_deep_stack(depth, lds_entries, out.ctypes.data) == 0
+    rank, tbits, tri_tests, box_tests = (int(v) for v in out)
+    # node 0's fourth child (leaf 2, or leaf 3 of a one-node comb) holds t = 1
+    assert rank == (2 if depth > 1 else 3), out
+    assert np.int32(tbits).view(np.float32) == np.float32(1.0)
+    assert tri_tests == 3 * depth + 1
+    assert box_tests == 1 + 4 * depth

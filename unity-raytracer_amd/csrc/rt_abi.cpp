@@ -140,6 +140,7 @@ int rt_export_bvh(const rt_ctx *ctx, void *nodes, void *triangle_records, void *
     info->sphere_records = ctx->sphere_count;
     DeviceGuard guard;
     if (hipSetDevice(ctx->device) != hipSuccess) return RT_E_HIP;
+    const Wait w("rt_export_bvh: hipMemcpy");
     if (nodes && info->nodes &&
         hipMemcpy(nodes, ctx->S.nodes4, sizeof(rtd::BvhNode4) * (size_t)info->nodes, hipMemcpyDeviceToHost) !=
             hipSuccess)
@@ -273,11 +274,11 @@ int rt_synchronize(rt_ctx *ctx) {
     if (!ctx) return RT_E_INVALID;
     DeviceGuard guard;
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     for (const GroupSlot &g : ctx->gslots)
         for (size_t i = 1; g.used && i < g.member_stream.size(); ++i) {
             HIP_OR_FAIL(ctx, hipSetDevice(member(ctx, (int)i)->device));
-            HIP_OR_FAIL(ctx, hipStreamSynchronize(g.member_stream[i]));
+            HIP_WAIT(ctx, hipStreamSynchronize(g.member_stream[i]));
         }
     return RT_OK;
 }
@@ -298,13 +299,13 @@ int rt_intersect_rays(rt_ctx *ctx, const rt_ray *rays, int32_t n, rt_hit *out_hi
         HIP_OR_FAIL(ctx, hipMalloc(&ctx->d_hits, (size_t)n * sizeof(int4)));
         ctx->rays_cap = (size_t)n;
     }
-    HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->d_rays, rays, (size_t)n * sizeof(rt_ray), hipMemcpyHostToDevice,
+    HIP_WAIT(ctx, hipMemcpyAsync(ctx->d_rays, rays, (size_t)n * sizeof(rt_ray), hipMemcpyHostToDevice,
                                     ctx->stream));
     HIP_OR_FAIL(ctx, rtk::launch_intersect(ctx->S, ctx->d_rays, n, ctx->d_hits, ctx->stream));
     std::vector<int4> hits((size_t)n);
-    HIP_OR_FAIL(ctx, hipMemcpyAsync(hits.data(), ctx->d_hits, (size_t)n * sizeof(int4), hipMemcpyDeviceToHost,
+    HIP_WAIT(ctx, hipMemcpyAsync(hits.data(), ctx->d_hits, (size_t)n * sizeof(int4), hipMemcpyDeviceToHost,
                                     ctx->stream));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     for (int32_t i = 0; i < n; ++i) {
         const int rk = hits[i].x;
         rt_hit &h = out_hits[i];
@@ -343,6 +344,10 @@ int rt_intersect_rays(rt_ctx *ctx, const rt_ray *rays, int32_t n, rt_hit *out_hi
 
 int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value) {
     if (!ctx) return RT_E_INVALID;
+    if (what == RT_DEBUG_GROUP_SAMPLE_WAVES) {
+        for (int i = 0; i < nmembers(ctx); ++i) member(ctx, i)->debug_group_sample_waves = value != 0;
+        return RT_OK;
+    }
     if (what == RT_DEBUG_FAIL_SLAB) {
         ctx->debug_fail_slab = value;
         return RT_OK;
@@ -357,16 +362,25 @@ int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value) {
 }
 
 int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, int64_t *bytes_written) {
-    if (!ctx) return RT_E_INVALID;
     if (bytes_written) *bytes_written = 0;
+    if (what == RT_DEBUG_HOST_WAITS) {
+        if (!out || capacity_bytes <= 0) return ctx ? fail(ctx, RT_E_INVALID, "rt_debug_read: no output") : RT_E_INVALID;
+        const std::string r = host_waits_report(ctx);
+        const int64_t n = std::min<int64_t>(capacity_bytes - 1, (int64_t)r.size());
+        std::memcpy(out, r.data(), (size_t)n);
+        static_cast<char *>(out)[n] = 0;
+        if (bytes_written) *bytes_written = n + 1;
+        return RT_OK;
+    }
+    if (!ctx) return RT_E_INVALID;
     if (what != RT_DEBUG_WAVE_CLOCKS) return fail(ctx, RT_E_INVALID, "unknown rt_debug_read item %d", what);
     if (!ctx->debug_wave_clock) return fail(ctx, RT_E_STATE, "RT_DEBUG_WAVE_CLOCKS is off");
     if (!out || capacity_bytes < 0) return fail(ctx, RT_E_INVALID, "rt_debug_read: null output or negative size");
     DeviceGuard guard;
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    HIP_OR_FAIL(ctx, hipDeviceSynchronize());
+    HIP_WAIT(ctx, hipDeviceSynchronize());
     const int64_t n = std::min<int64_t>(capacity_bytes, ctx->wave_clock_bytes);
-    if (n > 0) HIP_OR_FAIL(ctx, hipMemcpy(out, ctx->wave_clock.p, (size_t)n, hipMemcpyDeviceToHost));
+    if (n > 0) HIP_WAIT(ctx, hipMemcpy(out, ctx->wave_clock.p, (size_t)n, hipMemcpyDeviceToHost));
     if (bytes_written) *bytes_written = n;
     return RT_OK;
 }

@@ -187,7 +187,7 @@ int prepare_wavefront(rt_ctx *ctx, const rtd::FrameDev &F, int &chunk_tiles, rtw
     const size_t pool = tiles * 64 * levels, shadow = tiles * 64 * lights;
     if (!ctx->wf_ctr) HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ctr, sizeof(rtw::Counters)));
     if (pool > ctx->pool_cap || shadow > ctx->shadow_cap) {
-        HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
         free_wavefront(ctx);
         const size_t p = std::max(pool, ctx->pool_cap), q = std::max(shadow, ctx->shadow_cap);
         HIP_OR_FAIL(ctx, hipMalloc(&ctx->wf_ray_o, p * sizeof(float4)));
@@ -307,7 +307,7 @@ void read_folded(const rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords
 int read_counters(rt_ctx *ctx, unsigned long long counts[rtd::kCounterWords]) {
     int st = fold_counters(ctx, ctx->stream);
     if (st) return st;
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     read_folded(ctx, counts);
     return RT_OK;
 }
@@ -332,7 +332,7 @@ void fill_stats(rt_stats *stats, const unsigned long long counts[rtd::kCounterWo
 int settle_async(rt_ctx *ctx) {
     if (ctx->async_frames == 0) return RT_OK;
     // the pending frames may sit on several streams (rt_set_stream between them)
-    HIP_OR_FAIL(ctx, hipDeviceSynchronize());
+    HIP_WAIT(ctx, hipDeviceSynchronize());
     unsigned long long counts[rtd::kCounterWords];
     int st = read_counters(ctx, counts);
     if (st) return st;
@@ -383,6 +383,11 @@ static bool overlapped_frame(const rt_ctx *ctx, const rt_render_params *prm) {
         if (se.first && se.first != ctx->stream) return true;
     return false;
 }
+
+// One-sample waves in this frame's band: not in the bands of a multi-device
+// frame (rt_group.cpp group_frame) unless rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES)
+// asks for them (see lpt_prepare).
+static bool group_sample_waves(const rt_ctx *ctx) { return !ctx->in_group_frame || ctx->debug_group_sample_waves; }
 
 // Longest-first dispatch of a megakernel launch: picks the state of
 // (stream, slab), points F at the last measured order and decides whether
@@ -443,7 +448,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         if (kSplit16Div > 0 && 4 % F.spp == 0) {
             // a lone shard's (one-sample waves, below) twice as many: a 1/8
             // C3 share's single frame -11.9 %; in flight +2.6 % (r04av)
-            const bool sample_waves = F.spp == 4 && !overlapped_frame(ctx, prm) && !ctx->in_group_frame;
+            const bool sample_waves = F.spp == 4 && !overlapped_frame(ctx, prm) && group_sample_waves(ctx);
             const int div = sample_waves ? kSplit16Div / 2 : kSplit16Div;
             F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / div));
             F.split_tiles -= F.split16_tiles;
@@ -481,7 +486,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // and two full GPU-suite runs of 8-member groups on one device stalled
     // with them (r04s, r04an; cause not found, 5 other runs passed).
     if (F.split16_tiles > 0 && !count && !levels && F.spp == 4 && F.num_tiles <= rtk::kShardTilesMax &&
-        F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm) && !ctx->in_group_frame) {
+        F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm) && group_sample_waves(ctx)) {
         F.s16_shift = 0;
         const size_t sb = (size_t)F.split16_tiles * rtd::kWaveSize * 4 * sizeof(float);
         const size_t cb = (size_t)F.split16_tiles * (rtd::kWaveSize / 4) * sizeof(int);
@@ -737,9 +742,9 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             if (st) return st;
         }
         if (host_out && out_bytes)
-            HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_WAIT(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     }
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     unsigned long long counts[rtd::kCounterWords];
     read_folded(ctx, counts);
     if (stats) {

@@ -68,6 +68,7 @@ int create_one(int dev, rt_ctx **out) {
 
 void destroy_one(rt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
+    const Wait w("destroy: copier stop + stream synchronisations");
     ctx->copier.stop();
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
@@ -180,7 +181,11 @@ int create_group(const int32_t *devices, int32_t n, int32_t gather, rt_ctx **out
             return fail(nullptr, RT_E_NO_DEVICE, "RT_GATHER_RCCL: librccl.so.1 not loadable");
         }
         root->comms.assign((size_t)n, nullptr);
-        const ncclResult_t r = R.comm_init_all(root->comms.data(), n, devices);
+        ncclResult_t r;
+        {
+            const Wait w("ncclCommInitAll");
+            r = R.comm_init_all(root->comms.data(), n, devices);
+        }
         if (r != ncclSuccess) {
             root->comms.clear();
             release_group(root);
@@ -292,12 +297,12 @@ int copy_band_rows(rt_ctx *m, const void *band_buf, void *host, int res_x, int r
     const int full = res_y / R;                                   // whole blocks of the image
     const int mine = full > band ? (full - band + bands - 1) / bands : 0;  // ... that are this member's
     if (mine > 0 && row > 0)
-        HIP_OR_FAIL(m, hipMemcpy2DAsync((char *)host + (size_t)band * R * row, (size_t)bands * R * row, band_buf,
+        HIP_WAIT(m, hipMemcpy2DAsync((char *)host + (size_t)band * R * row, (size_t)bands * R * row, band_buf,
                                         (size_t)R * row, (size_t)R * row, (size_t)mine, hipMemcpyDeviceToHost,
                                         m->stream));
     const int rest = res_y - full * R;  // rows of a last partial block
     if (rest > 0 && full % bands == band && row > 0)
-        HIP_OR_FAIL(m, hipMemcpyAsync((char *)host + (size_t)full * R * row,
+        HIP_WAIT(m, hipMemcpyAsync((char *)host + (size_t)full * R * row,
                                       (const char *)band_buf + (size_t)(full / bands) * R * row, (size_t)rest * row,
                                       hipMemcpyDeviceToHost, m->stream));
     return RT_OK;
@@ -387,7 +392,7 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
         for (int i = 0; i < n; ++i) {
             rt_ctx *m = member(ctx, i);
             HIP_OR_FAIL(ctx, hipSetDevice(m->device));
-            HIP_OR_FAIL(ctx, hipStreamSynchronize(m->stream));
+            HIP_WAIT(ctx, hipStreamSynchronize(m->stream));
         }
         HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
         return group_stats(ctx, stash, stats, t0);
@@ -406,7 +411,11 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
             r = Rc.send(gs->member_out[0].p, shard, ncclChar, 0, ctx->comms[0], ctx->stream);
             if (r == ncclSuccess) r = Rc.recv(gs->gather.p, shard, ncclChar, 0, ctx->comms[0], ctx->stream);
         }
-        const ncclResult_t r2 = Rc.group_end();
+        ncclResult_t r2;
+        {
+            const Wait w("ncclGroupEnd (band gather)");
+            r2 = Rc.group_end();
+        }
         if (r != ncclSuccess || r2 != ncclSuccess)
             return fail(ctx, RT_E_HIP, "RCCL band gather: %s", Rc.error_string(r != ncclSuccess ? r : r2));
     } else {
@@ -428,12 +437,12 @@ int group_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, 
                                           px_bytes, d_out, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(gs->gather_free, ctx->stream));
     if (host_out && full_bytes)
-        HIP_OR_FAIL(ctx, hipMemcpyAsync(host_out, d_out, full_bytes, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_WAIT(ctx, hipMemcpyAsync(host_out, d_out, full_bytes, hipMemcpyDeviceToHost, ctx->stream));
     if (async) {
         if (stats) std::memset(stats, 0, sizeof *stats);
         return RT_OK;
     }
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     return group_stats(ctx, stash, stats, t0);
 }
 

@@ -174,6 +174,26 @@ struct GroupSlot {
     hipEvent_t gather_free = nullptr;        // device 0: the last frame's bands are reassembled
 };
 
+// Host waits (rt_debug_read RT_DEBUG_HOST_WAITS): every runtime call of the
+// library that can block its thread (synchronisations, copies into pageable
+// host memory, frees, the copier hand-off, RCCL group ends, thread joins)
+// runs inside a Wait scope, which records in its thread's slot of a fixed
+// table what the thread waits for and since when.  A report of that table
+// (and of the context's streams) names the call a stalled thread sits in.
+class Wait {
+  public:
+    explicit Wait(const char *what);
+    ~Wait();
+    Wait(const Wait &) = delete;
+    Wait &operator=(const Wait &) = delete;
+
+  private:
+    int slot_;
+    const char *prev_what_;
+    long long prev_since_;
+};
+std::string host_waits_report(rt_ctx *ctx);
+
 // rt_render's host-output copies, issued from a thread of their own: a copy
 // into pageable memory holds the calling thread until it is done, so the
 // thread that enqueues the slab launches must not be the one that copies — the
@@ -212,8 +232,11 @@ struct Copier {
             // the copy stream waits for the slab on the device; a pageable
             // copy returns once it is done
             hipError_t e = hipStreamWaitEvent(stream, j.ready, 0);
-            if (e == hipSuccess) e = hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToHost, stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            {
+                const Wait w("copier: slab copy into the host frame");
+                if (e == hipSuccess) e = hipMemcpyAsync(j.dst, j.src, j.bytes, hipMemcpyDeviceToHost, stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            }
             lk.lock();
             if (e != hipSuccess && err == hipSuccess) err = e;
             busy = false;
@@ -228,6 +251,7 @@ struct Copier {
         cv.notify_one();
     }
     hipError_t wait() {  // every posted copy is done; returns (and clears) the first error
+        const Wait w("copier.wait (posted slab copies)");
         std::unique_lock<std::mutex> lk(mu);
         done_cv.wait(lk, [this] { return jobs.empty() && !busy; });
         const hipError_t e = err;
@@ -241,6 +265,7 @@ struct Copier {
             quit = true;
         }
         cv.notify_all();
+        const Wait w("copier.stop join");
         th.join();
     }
 };
@@ -338,6 +363,7 @@ struct rt_ctx {
     // rt_debug_set(RT_DEBUG_WAVE_CLOCKS), measuring builds: the last render_kernel launch's per-wave clocks
     bool debug_wave_clock = false;
     bool in_group_frame = false;  // rendering one band of a multi-device frame (rt_group.cpp group_frame)
+    bool debug_group_sample_waves = false;  // rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES): testing only
     rti::GrowBuf wave_clock;
     int64_t wave_clock_bytes = 0;
 };
@@ -352,6 +378,18 @@ int fail(rt_ctx *ctx, int status, const char *fmt, ...);
 #define HIP_OR_FAIL(ctx, call)                                                                   \
     do {                                                                                         \
         hipError_t e_ = (call);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail((ctx), RT_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_));         \
+    } while (0)
+
+
+#define HIP_WAIT(ctx, call)                                                                      \
+    do {                                                                                         \
+        hipError_t e_;                                                                           \
+        {                                                                                        \
+            const rti::Wait w_(#call);                                                           \
+            e_ = (call);                                                                         \
+        }                                                                                        \
         if (e_ != hipSuccess)                                                                    \
             return fail((ctx), RT_E_HIP, "%s failed: %s", #call, hipGetErrorString(e_));         \
     } while (0)
@@ -418,7 +456,10 @@ int for_members(rt_ctx *ctx, Fn fn) {
     std::vector<std::thread> th;
     th.reserve((size_t)n);
     for (int i = 0; i < n; ++i) th.emplace_back([&, i] { st[(size_t)i] = fn(member(ctx, i)); });
-    for (auto &t : th) t.join();
+    {
+        const Wait w("for_members join");
+        for (auto &t : th) t.join();
+    }
     for (int i = 0; i < n; ++i)
         if (st[(size_t)i] != RT_OK) {
             if (i) ctx->err = "device " + std::to_string(member(ctx, i)->device) + ": " + member(ctx, i)->err;

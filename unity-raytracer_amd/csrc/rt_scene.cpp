@@ -21,6 +21,7 @@ void free_scene(rt_ctx *c) {
 template <typename T>
 hipError_t upload(void **dst, const std::vector<T> &v) {
     if (v.empty()) return hipSuccess;
+    const rti::Wait w("upload: hipMalloc + hipMemcpy");
     hipError_t e = hipMalloc(dst, v.size() * sizeof(T));
     if (e != hipSuccess) return e;
     return hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
@@ -110,6 +111,7 @@ template <typename T>
 hipError_t put(rt_ctx *ctx, GrowBuf &b, const T *src, size_t count) {
     hipError_t e = ensure(ctx, b, count * sizeof(T));
     if (e != hipSuccess || count == 0) return e;
+    const rti::Wait w("put: hipMemcpyAsync from pageable host memory");
     return hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
 }
 
@@ -164,12 +166,12 @@ int run_lbvh(rt_ctx *ctx, const rtl::LbvhInput &in, bool wide, rtd::SceneDev &S,
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     HIP_OR_FAIL(ctx, rtl::build_lbvh_gpu(in, out, B.scratch.p, B.scratch.cap, ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     float ms = 0.0f;
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->info.build_ms += ms;
     int binfo[3] = {0, 0, 0};  // 2-wide depth, 4-wide node count, 4-wide depth
-    HIP_OR_FAIL(ctx, hipMemcpy(binfo, rtl::lbvh_info_ptr(B.scratch.p, P), sizeof(binfo), hipMemcpyDeviceToHost));
+    HIP_WAIT(ctx, hipMemcpy(binfo, rtl::lbvh_info_ptr(B.scratch.p, P), sizeof(binfo), hipMemcpyDeviceToHost));
     ctx->last_bvh_depth = wide ? binfo[2] : binfo[0];
     // traversal stack: one entry per 2-wide level, three per 4-wide level
     const int need = wide ? 3 * (binfo[2] + 1) : binfo[0] + 1;
@@ -277,9 +279,9 @@ int extract_meshes(rt_ctx *ctx, std::vector<rtd::MeshGate> &aabbs, float &ms) {
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     aabbs.resize((size_t)a.mesh_count);
     if (a.mesh_count)
-        HIP_OR_FAIL(ctx, hipMemcpyAsync(aabbs.data(), B.src_aabbs.p, sizeof(rtd::MeshGate) * aabbs.size(),
+        HIP_WAIT(ctx, hipMemcpyAsync(aabbs.data(), B.src_aabbs.p, sizeof(rtd::MeshGate) * aabbs.size(),
                                         hipMemcpyDeviceToHost, ctx->stream));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     return RT_OK;
 }
@@ -311,7 +313,7 @@ int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geo
     if (mesh_ranks + sc->sphere_count + sc->triangle_count > (int64_t)(1 << rtd::kLeafFirstBits))
         return fail(ctx, RT_E_SCENE, "too many primitives (max %d)", 1 << rtd::kLeafFirstBits);
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     free_scene(ctx);
     ctx->info = rt_scene_info{};
     ++ctx->scene_version;
@@ -480,7 +482,7 @@ int set_scene_impl(rt_ctx *ctx, const rt_scene_desc *sc, int32_t build, bool geo
         const int st = enqueue_cut(ctx);
         if (st) return st;
     }
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
 
     S.leaves = nullptr;
     S.mats = (const rtd::DevMaterial *)ctx->arr.mats;
@@ -614,8 +616,8 @@ int refit_build(rt_ctx *ctx, const std::vector<rtd::MeshGate> &aabbs, bool host_
     if (host_sah && tt) {
         mtris.resize((size_t)tt);
         mnorm.resize((size_t)tt);
-        HIP_OR_FAIL(ctx, hipMemcpy(mtris.data(), B.mesh_tris.p, sizeof(rt_triangle) * (size_t)tt, hipMemcpyDeviceToHost));
-        HIP_OR_FAIL(ctx, hipMemcpy(mnorm.data(), B.mesh_normals.p, sizeof(rt_float3) * (size_t)tt,
+        HIP_WAIT(ctx, hipMemcpy(mtris.data(), B.mesh_tris.p, sizeof(rt_triangle) * (size_t)tt, hipMemcpyDeviceToHost));
+        HIP_WAIT(ctx, hipMemcpy(mnorm.data(), B.mesh_normals.p, sizeof(rt_float3) * (size_t)tt,
                                    hipMemcpyDeviceToHost));
     }
     for (int m = 0; m < M; ++m) {
@@ -666,7 +668,7 @@ int refit_build(rt_ctx *ctx, const std::vector<rtd::MeshGate> &aabbs, bool host_
     }
     HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->quality, a.quality, 2 * sizeof(float), hipMemcpyDeviceToHost,
                                     ctx->stream));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     const volatile float *q = ctx->h_update->quality;
     R.area_built = q[1] > 0.0f ? q[0] / q[1] : 0.0f;
     return RT_OK;
@@ -718,7 +720,7 @@ int set_scene_source_one(rt_ctx *ctx, const rt_scene_desc *base, const rt_mesh_s
         }
     }
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     LbvhBufs &B = ctx->lb;
     HIP_OR_FAIL(ctx, put(ctx, B.src_meshes, md.data(), md.size()));
     HIP_OR_FAIL(ctx, put(ctx, B.src_local, local.data(), local.size()));
@@ -792,7 +794,7 @@ int refit_update(rt_ctx *ctx, std::chrono::steady_clock::time_point t0) {
         HIP_OR_FAIL(ctx, hipMemcpyAsync(ctx->h_update->quality, a.quality, 2 * sizeof(float), hipMemcpyDeviceToHost,
                                         ctx->stream));
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     float xform_ms = 0.0f, refit_ms = 0.0f;
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&xform_ms, ctx->ev0, ctx->ev_x));
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&refit_ms, ctx->ev_x, ctx->ev1));
@@ -814,7 +816,7 @@ int refit_update(rt_ctx *ctx, std::chrono::steady_clock::time_point t0) {
         if (!(area <= limit * R.area_built)) {
             std::vector<rtd::MeshGate> aabbs((size_t)ctx->src.mesh_count);
             if (!aabbs.empty())
-                HIP_OR_FAIL(ctx, hipMemcpy(aabbs.data(), ctx->lb.src_aabbs.p, sizeof(rtd::MeshGate) * aabbs.size(),
+                HIP_WAIT(ctx, hipMemcpy(aabbs.data(), ctx->lb.src_aabbs.p, sizeof(rtd::MeshGate) * aabbs.size(),
                                            hipMemcpyDeviceToHost));
             const double build_ms = ctx->info.build_ms;
             const int st = refit_build(ctx, aabbs, false, t0);
@@ -850,7 +852,7 @@ int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t
         const int st = settle_async(ctx);
         if (st) return st;
     }
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     LbvhBufs &B = ctx->lb;
     if (!ctx->h_update)
         HIP_OR_FAIL(ctx, hipHostMalloc((void **)&ctx->h_update, sizeof *ctx->h_update, hipHostMallocCoherent));
@@ -890,7 +892,7 @@ int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t
         if (st) return st;
     }
     HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    HIP_OR_FAIL(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     float xform_ms = 0.0f, build_ms = 0.0f;
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&xform_ms, ctx->ev0, ctx->ev_x));
     HIP_OR_FAIL(ctx, hipEventElapsedTime(&build_ms, ctx->ev_x, ctx->ev1));

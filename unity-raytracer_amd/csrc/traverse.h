@@ -421,7 +421,9 @@ __device__ __forceinline__ bool traverse(const rtd::SceneDev &S, const RayCtx &r
         best_rank = -1;
         return false;
     }
-    const Stack st{wave_st.lds + lane_id(), wave_st.ovf};
+    // the instance's LDS depth travels with the stack (the 5-wave instances
+    // hold kStackShard entries in LDS and size their overflow for that)
+    const Stack st{wave_st.lds + lane_id(), wave_st.ovf, wave_st.n};
     while (!trav_step<ANY, COUNT, MESH_ONLY>(S, r, t, d2, st, cnt)) {
     }
     best_t = t.best_t;

@@ -11,6 +11,7 @@ path: constructing it without the HIP library raises.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 import math
 from typing import Optional
 
@@ -72,6 +73,24 @@ def frame_params(fr: Frame, **kw) -> abi.rt_render_params:
     return params_struct(fr.background, fr.max_bounces, kw.pop("spp", fr.spp), **kw)
 
 
+# every open Context (the stall watchdogs report on them)
+LIVE_CONTEXTS: "weakref.WeakSet[Context]" = weakref.WeakSet()
+
+
+def host_waits_report(ctx=None, lib=None) -> str:
+    """rt_debug_read(RT_DEBUG_HOST_WAITS): the library's host threads that sit
+    in a blocking runtime call right now (which call, for how long) and, for a
+    context, whether its streams still have work pending.  Callable from
+    another thread while a call of that context is blocked (the watchdog of
+    tests/conftest.py and tools/stall_probe.py)."""
+    lib = lib or abi.load_library()
+    buf = C.create_string_buffer(1 << 16)
+    n = C.c_int64(0)
+    h = ctx.h if ctx is not None else None
+    st = lib.rt_debug_read(h, abi.RT_DEBUG_HOST_WAITS, C.cast(buf, C.c_void_p), len(buf), C.byref(n))
+    return buf.value.decode(errors="replace") if st == abi.RT_OK else f"rt_debug_read: status {st}"
+
+
 class Context:
     """Owns one rt_ctx.  Thin, error-checked wrapper of the C-ABI.
 
@@ -91,6 +110,7 @@ class Context:
             raise abi.RtError(st, self.lib.rt_last_error(None).decode())
         self.h = h
         self._scene_desc = None
+        LIVE_CONTEXTS.add(self)
 
     def _check(self, st: int):
         if st != abi.RT_OK:
