@@ -152,16 +152,17 @@ def roofline(pmc, pmc_state, kernel_name, avg_kernel_s, logical):
     return out
 
 
-def trace_kernel_name(mode, spp, depth, res_x, local_rows):
+def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     """The trace kernel instance a frame launches (rtk::launch_render_mega and
-    lpt_prepare in csrc/trace.hip / csrc/rt_abi.cpp): the all-packet levels
+    lpt_prepare in csrc/trace.hip / csrc/rt_frame.cpp): the all-packet levels
     kernel for >= 16 spp, otherwise render_kernel<COUNT, SPLIT, DEEP, Q4, W> —
     SPLIT when the frame splits its slowest tiles — shards always (quarter-
     and sixteenth-waves up to 24,000 tiles, sixteenth-waves above), whole
-    frames when no frame of another stream runs beside them (lpt_prepare
-    overlapped_frame): the kernel-only frames below run back to back on one
-    stream, so they split — Q4 for 2x2 spp, W the waves per SIMD (5 for
-    shards of <= 70,000 tiles and deep frames, else 6)."""
+    frames only when no frame of another stream runs beside them (lpt_prepare
+    overlapped_frame; `in_flight` False: frames one at a time) — Q4 for 2x2
+    spp, W the waves per SIMD (5 for shards of <= 70,000 tiles and deep
+    frames, else 6).  The bench's timed frames are in flight (four streams):
+    whole frames run the non-split instance."""
     if mode == "packet":
         return "render_packet_kernel<false, true>"
     if mode == "wavefront":
@@ -174,7 +175,7 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows):
     th = 1 << (lg // 2) if ppw & (ppw - 1) == 0 else 1
     tw = ppw // th
     tiles = -(-res_x // tw) * -(-local_rows // th)
-    split = not deep and ((16 % spp == 0 and tiles <= 24000) or 4 % spp == 0)
+    split = not deep and ((16 % spp == 0 and tiles <= 24000) or (4 % spp == 0 and (tiles <= 70000 or not in_flight)))
     waves = 5 if deep or (split and tiles <= 70000) else 6
     b = lambda v: "true" if v else "false"  # noqa: E731
     return (f"render_kernel<false, {b(split)}, {b(deep)}, {b(spp == 4 and tw == 4 and th == 4 and not deep)}, "
@@ -578,11 +579,17 @@ def main():
     elapsed = time.perf_counter() - t0
     rays = st.primary_rays + st.shadow_rays + st.reflection_rays
     moot = int(st.shadow_rays_moot)  # counted in rays, answered without a traversal
-    # kernel-only device time of this rank's trace launch: the same frames
-    # back to back without the gather, HIP events on the context's stream
+    # device time of the timed frames: HIP events on the streams the trace
+    # kernels ran on, from the first timed frame's start to the last one's
+    # end (rt_finish) — with frames in flight, the device time per launch of
+    # the instance the timed frames run (the roofline's kernel time)
+    kernel_ms = st.kernel_ms
+    # a lone frame's kernel time (the same frames back to back on one stream,
+    # no gather): such frames split their slowest tiles, so this is the split
+    # instance — what one synchronous Update() frame costs
     for _ in range(args.steps):
         ctx.render_device(fr.camera, fr.plane, aparams, out.data_ptr(), nbytes)
-    kernel_ms = ctx.finish().kernel_ms
+    lone_kernel_ms = ctx.finish().kernel_ms
 
     # a moving camera (N = 1): every frame from another viewpoint, so the
     # longest-first order always comes from earlier, different frames
@@ -662,8 +669,8 @@ def main():
                 print(json.dumps(diag), file=sys.stderr, flush=True)
                 raise SystemExit("sharded frame differs from the single-rank frame")
     if dist_on:
-        t = torch.tensor([elapsed, float(rays), kernel_ms, float(scene_misses), float(moot)], dtype=torch.float64,
-                         device="cpu" if gloo else "cuda")
+        t = torch.tensor([elapsed, float(rays), kernel_ms, float(scene_misses), float(moot), lone_kernel_ms],
+                         dtype=torch.float64, device="cpu" if gloo else "cuda")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -672,13 +679,15 @@ def main():
         kernel_ms_max = float(tmax[2])
         scene_misses = int(t[3])
         moot = int(t[4])
+        lone_kernel_ms_max = float(tmax[5])
     else:
         kernel_ms_max = kernel_ms
+        lone_kernel_ms_max = lone_kernel_ms
 
     if rank == 0:
-        avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's own trace kernel, HIP events
+        avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's timed frames, HIP events
         pmc, pmc_state = load_pmc(args.config, lib_path, band_count)
-        kname = trace_kernel_name(args.mode, fr.spp, fr.max_bounces, rx, local_rows)
+        kname = trace_kernel_name(args.mode, fr.spp, fr.max_bounces, rx, local_rows, in_flight=nstreams > 1)
         rays_per_frame = rays // args.steps
         line = {
             "metric": METRIC,
@@ -715,7 +724,11 @@ def main():
                 "mrays_per_s_traversed": (rays - moot) / elapsed / 1e6,
                 "frames_in_flight": nstreams,
                 "frames_per_gather": G if dist_on else None,
+                # device time per timed frame (HIP events over the timed frames)
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
+                # one frame at a time (the split instance of a lone frame)
+                "lone_kernel_ms_per_frame": lone_kernel_ms_max / args.steps,
+                "lone_kernel": trace_kernel_name(args.mode, fr.spp, fr.max_bounces, rx, local_rows, in_flight=False),
                 # primary samples (W*H*spp of the frame, or of this band) per second
                 "msamples_per_s": rx * (local_rows if args.sim_bands else ry) * fr.spp * args.steps / elapsed / 1e6,
                 "end_to_end_ms_per_frame": e2e_ms,

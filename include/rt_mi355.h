@@ -441,6 +441,11 @@ float rt_spec_threshold(void);
  * the context and its members still has work pending.  Safe to call from
  * another thread while a call of the context is blocked; ctx may be NULL. */
 #define RT_DEBUG_HOST_WAITS 4
+/* Diagnostics: rt_debug_read(ctx, RT_DEBUG_LAST_LAUNCH, out, cap, &n) writes
+ * the kernel instance the context's last render launch ran and its split
+ * shape (tiles, split16 / split tiles, one-sample shift, rows, band), as
+ * NUL-terminated text — which instance a frame took (tests, bench.py). */
+#define RT_DEBUG_LAST_LAUNCH 5
 int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value);
 int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, int64_t *bytes_written);
 

@@ -19,6 +19,7 @@ import _rt_pkg  # noqa: E402
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 (MI355X) device")
+    config.addinivalue_line("markers", "fullsize: whole BASELINE-size frames against the oracle (GPU)")
 
 
 # Per-test stall watchdog (GPU tests): a test that runs longer than this is

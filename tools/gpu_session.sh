@@ -3,6 +3,7 @@
 # Stages (each step under its own time limit; the first failure ends the
 # session, so nothing more runs on the GPU after a fault, abort or time-out):
 #   probe    tools/stall_probe.py, 8-member groups with one-sample waves
+#   hunt     the GPU suite HUNT_RUNS times with one-sample waves in group bands
 #   tests    the GPU suite (per-test watchdog, tests/conftest.py)
 #   smoke    __graft_entry__.smoke()
 #   bench    the default bench line (python bench.py)
@@ -31,6 +32,16 @@ if has probe; then
   timeout -k 10 600 python -u tools/stall_probe.py --rounds ${PROBE_ROUNDS:-30} --sample-waves ${PROBE_SW:-1} \
     > $out/probe_$tag.log 2>&1 || fail probe $out/probe_$tag.log 60
   tail -1 $out/probe_$tag.log
+fi
+if has hunt; then
+  # the whole suite, repeatedly, with one-sample waves in the group frames'
+  # bands (the configuration of round 4's two stalled runs); a stall ends the
+  # run through the per-test watchdog with the library's host-wait report
+  for k in $(seq 1 ${HUNT_RUNS:-3}); do
+    RT_TEST_GROUP_SAMPLE_WAVES=1 RT_TEST_WATCHDOG_S=60 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v \
+      --timeout 120 --timeout-method thread > $out/hunt${k}_$tag.log 2>&1 || fail hunt$k $out/hunt${k}_$tag.log 80
+    tail -1 $out/hunt${k}_$tag.log
+  done
 fi
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \

@@ -1,0 +1,66 @@
+"""Per-launch device time of one kernel instance from a rocprofv3 kernel trace.
+
+    python tools/kt_span.py gpurun_out/kt_<tag> --kernel "render_kernel<false, false, false, true, 6>"
+
+With frames in flight (bench.py's four streams) the launches of the timed
+instance overlap: each dispatch's own duration (rocprofv3 --stats "average")
+includes the time it shares the CUs with its neighbours, so it exceeds the
+time a launch costs the device.  This prints, for every kernel whose name
+contains --kernel (or the largest one when omitted): the dispatch count, the
+mean and median dispatch duration, and the union of the dispatch intervals
+divided by the dispatch count — the device time per launch, the figure
+bench.py's roofline uses (`roofline.avg_kernel_ms`: HIP events over the timed
+frames / K).  One JSON line per kernel.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+from collections import defaultdict
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace_dir")
+    ap.add_argument("--kernel", default="")
+    ap.add_argument("--min-grid", type=int, default=0, help="ignore dispatches with a smaller grid (warm-up frames)")
+    a = ap.parse_args()
+    files = glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no *kernel_trace.csv under {a.trace_dir}")
+    iv = defaultdict(list)
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            name = row["Kernel_Name"]
+            if a.kernel and a.kernel not in name:
+                continue
+            grid = int(float(row.get("Grid_Size") or row.get("Grid_Size_X") or 0))
+            if grid < a.min_grid:
+                continue
+            iv[name].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]), grid))
+    for name, lst in sorted(iv.items(), key=lambda kv: -sum(e - s for s, e, _ in kv[1])):
+        big = max(g for _, _, g in lst)
+        lst = sorted((s, e) for s, e, g in lst if g == big)  # the workload's launches, not warm-up frames
+        durs = [(e - s) * 1e-6 for s, e in lst]
+        union, cur_s, cur_e = 0, None, None
+        for s, e in lst:
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    union += cur_e - cur_s
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            union += cur_e - cur_s
+        print(json.dumps({"kernel": name, "grid": big, "dispatches": len(lst),
+                          "mean_dispatch_ms": round(statistics.mean(durs), 5),
+                          "median_dispatch_ms": round(statistics.median(durs), 5),
+                          "union_ms_per_dispatch": round(union * 1e-6 / len(lst), 5)}))
+        if not a.kernel:
+            break
+
+
+if __name__ == "__main__":
+    main()

@@ -48,8 +48,11 @@ def main():
     ap.add_argument("--band", default="", help="i/n: render only row band i of n (8-row blocks): a light load")
     ap.add_argument("--rgb32f", action="store_true", help="float RGB output (the bench's shard format at N > 1)")
     ap.add_argument("--async-frames", action="store_true",
-                    help="timed frames with RT_FLAG_ASYNC, as bench.py times them (the same kernel instance: "
-                         "synchronous whole frames split their slowest tiles, asynchronous ones do not)")
+                    help="timed frames with RT_FLAG_ASYNC, as bench.py times them")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="--async-frames: rotate the frames over this many streams (frames in flight, as "
+                         "bench.py's timed frames: a whole frame then runs the non-split instance; on one "
+                         "stream it is a lone frame, which splits its slowest tiles)")
     a = ap.parse_args()
     rt = _rt_pkg.load()
     fr = rt.make(a.config)
@@ -92,9 +95,14 @@ def main():
             ks, ts = [], []
             if a.async_frames:
                 pa = rt.frame_params(fr, flags=flags | rt.abi.RT_FLAG_ASYNC, **bkw)
-                for _ in range(a.frames):
-                    ctx.render_device(fr.camera, fr.plane, pa, out.data_ptr(), out.numel() * 4)
+                ss = [torch.cuda.Stream() for _ in range(max(1, a.streams))]
+                oo = [out] + [torch.empty_like(out) for _ in ss[1:]]
+                for k in range(a.frames):
+                    ctx.set_stream(ss[k % len(ss)].cuda_stream)
+                    ctx.render_device(fr.camera, fr.plane, pa, oo[k % len(ss)].data_ptr(), out.numel() * 4)
                 st = ctx.finish()
+                torch.cuda.synchronize()
+                ctx.set_stream(None)
                 for f_ in ("primary_rays", "shadow_rays", "reflection_rays"):
                     setattr(st, f_, getattr(st, f_) // a.frames)
                 ks.append(st.kernel_ms / a.frames)

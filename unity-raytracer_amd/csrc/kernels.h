@@ -39,8 +39,10 @@ hipError_t launch_build_cut(const rtd::BvhNode4 *nodes, rtd::CutTable *out, hipS
 // the same cut with its boxes re-read from the (refitted) tree
 hipError_t launch_refresh_cut(const rtd::BvhNode4 *nodes, rtd::CutTable *out, hipStream_t stream);
 
+// *instance (nullable): the name of the kernel instance launched (static
+// storage; null when nothing was launched) — rt_debug_read RT_DEBUG_LAST_LAUNCH.
 hipError_t launch_render_mega(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
-                              hipStream_t stream);
+                              hipStream_t stream, const char **instance = nullptr);
 
 // Level-synchronous all-packet megakernel (trace_levels.hip), chosen by
 // launch_render_mega for >= 16 spp on a 4-wide BVH.

@@ -373,6 +373,15 @@ int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, 
         return RT_OK;
     }
     if (!ctx) return RT_E_INVALID;
+    if (what == RT_DEBUG_LAST_LAUNCH) {
+        if (!out || capacity_bytes <= 0) return fail(ctx, RT_E_INVALID, "rt_debug_read: no output");
+        const std::string &r = ctx->last_launch;
+        const int64_t n = std::min<int64_t>(capacity_bytes - 1, (int64_t)r.size());
+        std::memcpy(out, r.data(), (size_t)n);
+        static_cast<char *>(out)[n] = 0;
+        if (bytes_written) *bytes_written = n + 1;
+        return RT_OK;
+    }
     if (what != RT_DEBUG_WAVE_CLOCKS) return fail(ctx, RT_E_INVALID, "unknown rt_debug_read item %d", what);
     if (!ctx->debug_wave_clock) return fail(ctx, RT_E_STATE, "RT_DEBUG_WAVE_CLOCKS is off");
     if (!out || capacity_bytes < 0) return fail(ctx, RT_E_INVALID, "rt_debug_read: null output or negative size");

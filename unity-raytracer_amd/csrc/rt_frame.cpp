@@ -558,8 +558,17 @@ Path frame_path(const rt_ctx *ctx, const rt_render_params *prm) {
 int launch_frame(rt_ctx *ctx, rtd::FrameDev &F, const Path &P, const rtw::Args &A, int chunk_tiles) {
     if (P.packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, P.count, ctx->stream));
-    else if (P.mega)
-        HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, P.count, ctx->stream));
+    else if (P.mega) {
+        const char *inst = nullptr;
+        HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, P.count, ctx->stream, &inst));
+        if (inst) {  // rt_debug_read RT_DEBUG_LAST_LAUNCH
+            char b[256];
+            snprintf(b, sizeof b, "%s tiles=%d split16=%d split=%d s16_shift=%d rows=%d band=%d/%d", inst,
+                     F.num_tiles, F.split16_tiles, F.split_tiles, F.s16_shift, F.local_rows, F.band_index,
+                     F.band_count);
+            ctx->last_launch = b;
+        }
+    }
     else if (P.wavefront && F.num_tiles > 0)
         HIP_OR_FAIL(ctx, rtk::launch_render_wavefront(ctx->S, F, A, chunk_tiles, P.count, ctx->stream));
     return RT_OK;

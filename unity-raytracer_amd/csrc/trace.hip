@@ -826,7 +826,11 @@ hipError_t launch_refresh_cut(const BvhNode4 *nodes, CutTable *out, hipStream_t 
 constexpr int kLevelsMinSpp = 16;
 
 
-hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_tests, hipStream_t stream) {
+hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_tests, hipStream_t stream,
+                              const char **instance) {
+    const char *dummy = nullptr;
+    const char *&name = instance ? *instance : dummy;
+    name = nullptr;
     if (F0.num_tiles <= 0) return hipSuccess;
     FrameDev F = F0;
     F.primary_total = active_samples(F.res_x, F.res_y, F.local_rows, F.row0, F.band_index, F.band_count, F.band_rows,
@@ -834,29 +838,32 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     int blocks = (render_mega_waves(F) + kMkWaves - 1) / kMkWaves;
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     const bool shard = F.num_tiles <= kShardTiles;  // a small frame: its slowest waves set its time
+    const bool split = F.split_tiles > 0 || F.split16_tiles > 0;
     constexpr int W5 = kMkMinWavesShard;
+    static_assert(kMkMinWaves == 6 && W5 == 5, "instance names below");
+#define RT_LAUNCH(K, NAME)                                                                  \
+    do {                                                                                    \
+        hipLaunchKernelGGL(K, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);             \
+        name = NAME;                                                                        \
+    } while (0)
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)
-            hipLaunchKernelGGL((render_kernel<true, false, true, false, W5>), dim3(blocks), dim3(kMkThreads), 0, stream,
-                               S, F);
+            RT_LAUNCH((render_kernel<true, false, true, false, W5>), "render_kernel<true, false, true, false, 5>");
         else
-            hipLaunchKernelGGL((render_kernel<false, false, true, false, W5>), dim3(blocks), dim3(kMkThreads), 0,
-                               stream, S, F);
+            RT_LAUNCH((render_kernel<false, false, true, false, W5>), "render_kernel<false, false, true, false, 5>");
     } else if (count_tests)
-        hipLaunchKernelGGL((render_kernel<true, false, false, false, W5>), dim3(blocks), dim3(kMkThreads), 0, stream, S,
-                           F);
-    else if ((F.split_tiles > 0 || F.split16_tiles > 0) && q4 && shard)
-        hipLaunchKernelGGL((render_kernel<false, true, false, true, W5>), dim3(blocks), dim3(kMkThreads), 0, stream, S,
-                           F);
-    else if ((F.split_tiles > 0 || F.split16_tiles > 0) && q4)
-        hipLaunchKernelGGL((render_kernel<false, true, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
-    else if ((F.split_tiles > 0 || F.split16_tiles > 0) && shard)
-        hipLaunchKernelGGL((render_kernel<false, true, false, false, W5>), dim3(blocks), dim3(kMkThreads), 0, stream, S,
-                           F);
-    else if (F.split_tiles > 0 || F.split16_tiles > 0)
-        hipLaunchKernelGGL((render_kernel<false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+        RT_LAUNCH((render_kernel<true, false, false, false, W5>), "render_kernel<true, false, false, false, 5>");
+    else if (split && q4 && shard)
+        RT_LAUNCH((render_kernel<false, true, false, true, W5>), "render_kernel<false, true, false, true, 5>");
+    else if (split && q4)
+        RT_LAUNCH((render_kernel<false, true, false, true>), "render_kernel<false, true, false, true, 6>");
+    else if (split && shard)
+        RT_LAUNCH((render_kernel<false, true, false, false, W5>), "render_kernel<false, true, false, false, 5>");
+    else if (split)
+        RT_LAUNCH((render_kernel<false, true>), "render_kernel<false, true, false, false, 6>");
     else if (S.bvh4 && F.spp >= kLevelsMinSpp) {
         const hipError_t e = launch_render_levels(S, F, stream);
+        name = F.spp <= 16 ? "render_levels_kernel<6>" : "render_levels_kernel<8>";
         if (e != hipSuccess || !F.wave_counts) return e;
         const int waves = F.num_tiles;  // one wave per tile, no splits
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
@@ -864,9 +871,10 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         return hipGetLastError();
     }
     else if (q4)
-        hipLaunchKernelGGL((render_kernel<false, false, false, true>), dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+        RT_LAUNCH((render_kernel<false, false, false, true>), "render_kernel<false, false, false, true, 6>");
     else
-        hipLaunchKernelGGL(render_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);
+        RT_LAUNCH(render_kernel<false>, "render_kernel<false, false, false, false, 6>");
+#undef RT_LAUNCH
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,

@@ -133,6 +133,15 @@ class Context:
         return {"num_devices": info.num_devices, "gather": info.gather,
                 "devices": list(info.devices)[:min(16, info.num_devices)]}
 
+    def last_launch(self) -> str:
+        """The kernel instance of the context's last render launch and its
+        split shape (rt_debug_read RT_DEBUG_LAST_LAUNCH)."""
+        buf = C.create_string_buffer(512)
+        n = C.c_int64(0)
+        self._check(self.lib.rt_debug_read(self.h, abi.RT_DEBUG_LAST_LAUNCH, C.cast(buf, C.c_void_p), len(buf),
+                                           C.byref(n)))
+        return buf.value.decode()
+
     def set_stream(self, stream_handle: int):
         self._check(self.lib.rt_set_stream(self.h, C.c_void_p(stream_handle)))
 
