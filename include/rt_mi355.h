@@ -429,10 +429,11 @@ float rt_spec_threshold(void);
  * measuring build is compiled with -DRT_WAVE_CLOCK.  One
  * frame in flight at a time: every launch overwrites the records. */
 #define RT_DEBUG_WAVE_CLOCKS 2
-/* Testing only: RT_DEBUG_GROUP_SAMPLE_WAVES (value 1: on) lets the bands of
- * this multi-device context's frames run their slowest pixels as one-sample
- * waves, which its frames otherwise never do (rt_frame.cpp lpt_prepare); the
- * stall probe (tools/stall_probe.py) uses it to exercise that configuration. */
+/* Testing only: RT_DEBUG_GROUP_SAMPLE_WAVES (value 0: off, 1: on, the
+ * default) — whether the bands of this multi-device context's frames may run
+ * a lone band's slowest pixels as one-sample waves (rt_frame.cpp
+ * lpt_prepare), as a single-device frame's small shards do; the stall probe
+ * (tools/stall_probe.py) and A/B runs switch it. */
 #define RT_DEBUG_GROUP_SAMPLE_WAVES 3
 /* Diagnostics: rt_debug_read(ctx, RT_DEBUG_HOST_WAITS, out, cap, &n) writes
  * a text report (NUL-terminated, truncated to cap) of every host thread that

@@ -14,15 +14,15 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-# Stall hunting only (tools/gpu_session.sh probe stage): the group frames'
-# bands take one-sample waves, as in round 4's two stalled suite runs.
-SAMPLE_WAVES = os.environ.get("RT_TEST_GROUP_SAMPLE_WAVES") == "1"
+# The group frames' bands take one-sample waves by default (round 5; round 4
+# kept them out after two stalled suite runs); RT_TEST_GROUP_SAMPLE_WAVES=0
+# runs the group tests without them (rt_debug_set RT_DEBUG_GROUP_SAMPLE_WAVES).
+SAMPLE_WAVES = os.environ.get("RT_TEST_GROUP_SAMPLE_WAVES", "1")
 
 
 def _group(rt, devices, gather=1):
     ctx = rt.Context(devices=devices, gather=gather)
-    if SAMPLE_WAVES:
-        assert ctx.lib.rt_debug_set(ctx.h, rt.abi.RT_DEBUG_GROUP_SAMPLE_WAVES, 1) == 0
+    assert ctx.lib.rt_debug_set(ctx.h, rt.abi.RT_DEBUG_GROUP_SAMPLE_WAVES, int(SAMPLE_WAVES)) == 0
     return ctx
 
 
@@ -183,3 +183,25 @@ def test_full_size_slabbed_host_frame_equals_device_frame(gpu_ctx, rt):
     torch.cuda.synchronize()
     assert np.array_equal(img.view(np.uint32), dev.cpu().numpy().view(np.uint32))
     assert _rays(st) == _rays(st2)
+
+
+def test_group_bands_take_one_sample_waves(gpu_ctx, rt):
+    """A synchronous frame's bands are lone shards: from the second frame on
+    (a measured tile order) their slowest pixels run as one-sample waves
+    (s16_shift 0, rt_debug_read RT_DEBUG_LAST_LAUNCH) — unless switched off —
+    and the frames stay bit-identical to the one-device frame."""
+    fr = _frame(rt, "C3", (480, 270))
+    ref, sref = _single(gpu_ctx, rt, fr)
+    for on in (1, 0):
+        ctx = rt.Context(devices=[0] * 4, gather=1)
+        try:
+            assert ctx.lib.rt_debug_set(ctx.h, rt.abi.RT_DEBUG_GROUP_SAMPLE_WAVES, on) == 0
+            ctx.set_scene(fr.scene)
+            for _ in range(3):
+                img, st = ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+                assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), on
+                assert _rays(st) == _rays(sref)
+            launch = ctx.last_launch()
+            assert "band=0/4" in launch and ("s16_shift=0" in launch) == bool(on), launch
+        finally:
+            ctx.close()

@@ -384,9 +384,17 @@ static bool overlapped_frame(const rt_ctx *ctx, const rt_render_params *prm) {
     return false;
 }
 
-// One-sample waves in this frame's band: not in the bands of a multi-device
-// frame (rt_group.cpp group_frame) unless rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES)
-// asks for them (see lpt_prepare).
+// One-sample waves in this frame's band.  The bands of a multi-device frame
+// (rt_group.cpp group_frame) take them too since round 5: round 4 had kept
+// them out after two stalled GPU-suite runs in the 8-member group tests
+// (r04s, r04an; cause not found then).  Round 5 re-ran that configuration —
+// four whole GPU suites and 230 stall-probe rounds (tools/stall_probe.py,
+// about 5,000 group contexts) — with no stall and bit-identical frames, after
+// fixing the lane stack of the 5-wave instances (traverse() had dropped its
+// LDS depth); tests/conftest.py's watchdog and rt_debug_read
+// RT_DEBUG_HOST_WAITS now name the blocking call should a stall recur.
+// rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0) keeps a context's group bands
+// on one-pixel waves.
 static bool group_sample_waves(const rt_ctx *ctx) { return !ctx->in_group_frame || ctx->debug_group_sample_waves; }
 
 // Longest-first dispatch of a megakernel launch: picks the state of
@@ -481,10 +489,9 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // them hides their slowest chain): a 1/8 C3 shard's single frame -20 %, a
     // 1/4 shard's -15 %; a lone 1/2 shard +5 %, whole frames +6 %; with four
     // frames in flight a 1/8 shard's throughput is -3 % to +-0 (r04r, r04ag,
-    // r04ai, 200-frame runs alternated on one box).  Not in the bands of a
-    // multi-device frame (rt_group.cpp): its members' frames run side by side,
-    // and two full GPU-suite runs of 8-member groups on one device stalled
-    // with them (r04s, r04an; cause not found, 5 other runs passed).
+    // r04ai, 200-frame runs alternated on one box).  The bands of a multi-device
+    // frame too, unless rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0)
+    // (group_sample_waves above).
     if (F.split16_tiles > 0 && !count && !levels && F.spp == 4 && F.num_tiles <= rtk::kShardTilesMax &&
         F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm) && group_sample_waves(ctx)) {
         F.s16_shift = 0;

@@ -363,7 +363,7 @@ struct rt_ctx {
     // rt_debug_set(RT_DEBUG_WAVE_CLOCKS), measuring builds: the last render_kernel launch's per-wave clocks
     bool debug_wave_clock = false;
     bool in_group_frame = false;  // rendering one band of a multi-device frame (rt_group.cpp group_frame)
-    bool debug_group_sample_waves = false;  // rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES): testing only
+    bool debug_group_sample_waves = true;  // rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0): group bands without them
     std::string last_launch;  // the last render launch's kernel instance and split shape (RT_DEBUG_LAST_LAUNCH)
     rti::GrowBuf wave_clock;
     int64_t wave_clock_bytes = 0;
