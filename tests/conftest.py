@@ -32,21 +32,49 @@ def pytest_configure(config):
 WATCHDOG_S = float(os.environ.get("RT_TEST_WATCHDOG_S", "100"))
 
 
+def _task_states():
+    """Every thread of this process as the kernel sees it: name, state and
+    wait channel (futex, an amdgpu/kfd wait, ...)."""
+    out = []
+    for tid in sorted(os.listdir("/proc/self/task"), key=int):
+        base = f"/proc/self/task/{tid}/"
+        try:
+            comm = open(base + "comm").read().strip()
+            state = open(base + "stat").read().rsplit(")", 1)[1].split()[0]
+            wchan = open(base + "wchan").read().strip() or "-"
+            sysc = open(base + "syscall").read().split()[0]
+        except OSError:
+            continue
+        out.append(f"  tid {tid} {comm!r} state {state} wchan {wchan} syscall {sysc}")
+    return "\n".join(out)
+
+
 def _stall_dump(name):
-    err = sys.__stderr__
+    # pytest captures fd 2 during a test: the dump goes to a file of its own
+    # (gpurun_out/ travels back from the GPU box) and to the terminal writer's fd
+    path = os.path.join(ROOT, "gpurun_out", f"stall_{os.getpid()}.txt")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    f = open(path, "w")
+
+    def out(text):
+        f.write(text + "\n")
+        f.flush()
+
+    out(f"=== watchdog: {name} still running after {WATCHDOG_S:.0f} s ===")
     try:
-        err.write(f"\n=== watchdog: {name} still running after {WATCHDOG_S:.0f} s ===\n")
-        err.flush()
         rtmod = sys.modules.get("unity_raytracer_amd.raytracing") or _rt_pkg.load().raytracing
-        ctxs = [c for c in list(rtmod.LIVE_CONTEXTS) if getattr(c, "h", None)]
-        err.write(rtmod.host_waits_report(None) + "\n")
-        for c in ctxs:
-            err.write(rtmod.host_waits_report(c) + "\n")
-        err.flush()
+        out(rtmod.host_waits_report(None))
+        out("threads (kernel view):\n" + _task_states())
+        for c in [c for c in list(rtmod.LIVE_CONTEXTS) if getattr(c, "h", None)]:
+            out(rtmod.host_waits_report(c))
     except Exception as e:  # the dump must not hide the stall itself
-        err.write(f"(library report failed: {e!r})\n")
-    faulthandler.dump_traceback(file=err, all_threads=True)
-    err.flush()
+        out(f"(library report failed: {e!r})")
+    faulthandler.dump_traceback(file=f, all_threads=True)
+    f.close()
+    try:
+        os.write(2, open(path, "rb").read())
+    except OSError:
+        pass
     os._exit(70)
 
 

@@ -59,6 +59,7 @@ int rt_get_device_info(const rt_ctx *ctx, rt_device_info *info) {
 void rt_destroy(rt_ctx *ctx) {
     if (!ctx) return;
     DeviceGuard guard;
+    ctx->destroying.store(true);  // host_waits_report no longer reads the context
     release_group(ctx);
     destroy_one(ctx);
 }

@@ -68,40 +68,58 @@ int create_one(int dev, rt_ctx **out) {
 
 void destroy_one(rt_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
-    const Wait w("destroy: copier stop + stream synchronisations");
-    ctx->copier.stop();
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
-    if (ctx->slab_stream2) (void)hipStreamSynchronize(ctx->slab_stream2);
-    free_scene(ctx);
-    free_wavefront(ctx);
-    ctx->lb.release();
-    ctx->src.refit.release();
-    for (LptSlot &l : ctx->lpt) l.release();
-    if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
-    if (ctx->d_out) (void)hipFree(ctx->d_out);
-    if (ctx->d_counters) (void)hipFree(ctx->d_counters);
-    if (ctx->d_cut) (void)hipFree(ctx->d_cut);
-    if (ctx->wave_clock.p) (void)hipFree(ctx->wave_clock.p);
-    if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
-    if (ctx->h_update) (void)hipHostFree(ctx->h_update);
-    if (ctx->ev_x) (void)hipEventDestroy(ctx->ev_x);
-    if (ctx->d_rays) (void)hipFree(ctx->d_rays);
-    if (ctx->d_hits) (void)hipFree(ctx->d_hits);
-    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
-    if (ctx->ev_a0) (void)hipEventDestroy(ctx->ev_a0);
-    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
-    if (ctx->ev_slab0) (void)hipEventDestroy(ctx->ev_slab0);
-    for (auto &se : ctx->async_end) (void)hipEventDestroy(se.second);
-    for (hipEvent_t e : ctx->slab_done) (void)hipEventDestroy(e);
-    if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
-    if (ctx->slab_stream2) (void)hipStreamDestroy(ctx->slab_stream2);
-    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    {
+        const Wait w("destroy: copier thread stop (join)");
+        ctx->copier.stop();
+    }
+    {
+        const Wait w("destroy: hipStreamSynchronize (stream, copy stream, slab stream)");
+        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+        if (ctx->slab_stream2) (void)hipStreamSynchronize(ctx->slab_stream2);
+    }
+    {
+        const Wait w("destroy: hipFree of scene, LBVH, refit and longest-first buffers");
+        free_scene(ctx);
+        free_wavefront(ctx);
+        ctx->lb.release();
+        ctx->src.refit.release();
+        for (LptSlot &l : ctx->lpt) l.release();
+        if (ctx->wf_ctr) (void)hipFree(ctx->wf_ctr);
+        if (ctx->d_out) (void)hipFree(ctx->d_out);
+        if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+        if (ctx->d_cut) (void)hipFree(ctx->d_cut);
+        if (ctx->wave_clock.p) (void)hipFree(ctx->wave_clock.p);
+        if (ctx->d_rays) (void)hipFree(ctx->d_rays);
+        if (ctx->d_hits) (void)hipFree(ctx->d_hits);
+    }
+    {
+        const Wait w("destroy: hipHostFree (counter and update words)");
+        if (ctx->h_counts) (void)hipHostFree(ctx->h_counts);
+        if (ctx->h_update) (void)hipHostFree(ctx->h_update);
+    }
+    {
+        const Wait w("destroy: hipEventDestroy");
+        if (ctx->ev_x) (void)hipEventDestroy(ctx->ev_x);
+        if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+        if (ctx->ev_a0) (void)hipEventDestroy(ctx->ev_a0);
+        if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+        if (ctx->ev_slab0) (void)hipEventDestroy(ctx->ev_slab0);
+        for (auto &se : ctx->async_end) (void)hipEventDestroy(se.second);
+        for (hipEvent_t e : ctx->slab_done) (void)hipEventDestroy(e);
+    }
+    {
+        const Wait w("destroy: hipStreamDestroy");
+        if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+        if (ctx->slab_stream2) (void)hipStreamDestroy(ctx->slab_stream2);
+        if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    }
     delete ctx;
 }
 
 void release_group(rt_ctx *ctx) {
     if (!ctx->comms.empty()) {  // only an RCCL group ever loaded the library
+        const Wait w("destroy: ncclCommDestroy");
         Rccl &R = rccl();
         for (ncclComm_t c : ctx->comms)
             if (c && R.ok) (void)R.comm_destroy(c);
@@ -113,13 +131,19 @@ void release_group(rt_ctx *ctx) {
         for (int i = 0; i < n && i < (int)g.member_stream.size(); ++i) {
             (void)hipSetDevice(member(ctx, i)->device);
             if (g.member_stream[(size_t)i]) {
-                (void)hipStreamSynchronize(g.member_stream[(size_t)i]);
+                {
+                    const Wait w("destroy: hipStreamSynchronize (a group band stream)");
+                    (void)hipStreamSynchronize(g.member_stream[(size_t)i]);
+                }
+                const Wait w("destroy: hipStreamDestroy (a group band stream)");
                 (void)hipStreamDestroy(g.member_stream[(size_t)i]);
             }
+            const Wait w("destroy: hipEventDestroy / hipFree (a group band's event and buffer)");
             if (g.member_done[(size_t)i]) (void)hipEventDestroy(g.member_done[(size_t)i]);
             if (g.member_out[(size_t)i].p) (void)hipFree(g.member_out[(size_t)i].p);
         }
         (void)hipSetDevice(ctx->device);
+        const Wait w("destroy: hipFree / hipEventDestroy (the group's gather buffer and event)");
         if (g.gather.p) (void)hipFree(g.gather.p);
         if (g.gather_free) (void)hipEventDestroy(g.gather_free);
         g = GroupSlot{};

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include <dlfcn.h>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -364,6 +365,7 @@ struct rt_ctx {
     bool debug_wave_clock = false;
     bool in_group_frame = false;  // rendering one band of a multi-device frame (rt_group.cpp group_frame)
     bool debug_group_sample_waves = true;  // rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0): group bands without them
+    std::atomic<bool> destroying{false};  // rt_destroy has begun (host_waits_report skips the context)
     std::string last_launch;  // the last render launch's kernel instance and split shape (RT_DEBUG_LAST_LAUNCH)
     rti::GrowBuf wave_clock;
     int64_t wave_clock_bytes = 0;

@@ -100,6 +100,7 @@ std::string host_waits_report(rt_ctx *ctx) {
     }
     if (!n) o += "  (none)\n";
     if (!ctx) return o;
+    if (ctx->destroying.load()) return o + "context: being destroyed (rt_destroy), not read\n";
     DeviceGuard guard;
     o += "streams of the context:\n";
     for (int m = 0; m < nmembers(ctx); ++m) {

@@ -218,6 +218,16 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
 }
 
 
+// The first hit's shadow packets keep the lane's hit and colours in LDS (the
+// lane stack's column, 16 entries) rather than in registers across the packet
+// loop (measuring builds: -DRT_EXP_STASH; A/B pending).
+#ifdef RT_EXP_STASH
+constexpr bool kShadowStash = true;
+#else
+constexpr bool kShadowStash = false;
+#endif
+static_assert(kStackSize >= 16, "the shadow-packet stash takes 16 lane-stack entries");
+
 // Shade (RayTracingSetup.cs:304-366) of one camera sample.  The first hit is
 // traced and shaded with wave packets (camera rays of a tile, then their
 // shadow rays to each light: packet.h, scalar node fetches); the mirror
@@ -242,12 +252,12 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     int *const hints = HINT && F.shadow_hint ? F.shadow_hint + (size_t)tile * kHintLights : nullptr;
     int4 hv = make_int4(0, 0, 0, 0);
     if (HINT && hints) hv = rtt::cload(reinterpret_cast<const int4 *>(hints));
-    const rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
+    rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
         const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
         // a moot shadow ray (shade.h same_bits) is not traced
-        const f3 lit = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+        f3 lit = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
         const bool moot = rts::same_bits(lit, col);
         cnt.shadow++;
         cnt.moot += moot;
@@ -257,8 +267,30 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
         RT_SEG(const unsigned long long tw0 = __builtin_amdgcn_s_memtime();)
         const bool hl = HINT && hints && l < kHintLights;
         const int h = !hl ? 0 : l == 0 ? hv.x : l == 1 ? hv.y : l == 2 ? hv.z : hv.w;
-        rtp::packet_trace<true, COUNT, HINT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr, h,
-                                             hl ? hints + l : nullptr);
+        if (kShadowStash) {
+            // the hit and both colours wait in the lane's LDS stack column
+            // (unused by packets; the mirror chain's per-lane walks come after
+            // the last light) instead of in registers the packet loop needs
+            volatile int *vs = st.lds + rtt::lane_id();
+            const float v[15] = {sf.p.x, sf.p.y, sf.p.z, sf.n.x, sf.n.y, sf.n.z, sf.view.x, sf.view.y, sf.view.z,
+                                 col.x, col.y, col.z, lit.x, lit.y, lit.z};
+#pragma unroll
+            for (int i = 0; i < 15; ++i) vs[i * kWaveSize] = __float_as_int(v[i]);
+            vs[15 * kWaveSize] = sf.mat;
+            rtp::packet_trace<true, COUNT, HINT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr,
+                                                 h, hl ? hints + l : nullptr);
+            vs = st.lds + rtt::lane_id();
+            auto ld = [&](int i) { return __int_as_float(vs[i * kWaveSize]); };
+            sf.p = mk(ld(0), ld(1), ld(2));
+            sf.n = mk(ld(3), ld(4), ld(5));
+            sf.view = mk(ld(6), ld(7), ld(8));
+            col = mk(ld(9), ld(10), ld(11));
+            lit = mk(ld(12), ld(13), ld(14));
+            sf.mat = vs[15 * kWaveSize];
+        } else {
+            rtp::packet_trace<true, COUNT, HINT>(S, rs, !moot, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack, cnt, nullptr,
+                                                 h, hl ? hints + l : nullptr);
+        }
         RT_SEG(sg.shadow += __builtin_amdgcn_s_memtime() - tw0;
                sg.visits += Q.nodes + ((unsigned long long)Q.leaves << 32);)
         if (moot || Q.best_rank == 1) continue;
