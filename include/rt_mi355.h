@@ -191,7 +191,14 @@ typedef struct rt_stats {
                                   cannot change the pixel — the light's unoccluded
                                   term leaves the colour's bits unchanged, e.g. a
                                   light behind the surface — so they were not
-                                  traversed (0 in RT_FLAG_COUNT_TESTS frames)      */
+                                  traversed (0 in RT_FLAG_COUNT_TESTS frames).
+                                  Which moot rays are skipped depends on how the
+                                  frame was dispatched: every packet traversal
+                                  skips them, the per-lane mirror chains only in
+                                  split tiles — so a frame that splits its slowest
+                                  tiles may report more than the same frame
+                                  unsplit; pixels and every other count are
+                                  the same                                         */
 } rt_stats;
 
 /* Closest-hit record, IntersectionResult (Data/Collision/IntersectionResult.cs:3-7)

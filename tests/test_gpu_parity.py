@@ -322,6 +322,11 @@ def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
             assert np.array_equal(img.view(np.uint32), row.view(np.uint32)), kw
             assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == (sr.primary_rays, sr.shadow_rays,
                                                                              sr.reflection_rays), kw
+            # shadow_rays_moot counts the moot rays a frame did not traverse:
+            # the split tiles' per-lane mirror chains skip theirs, whole tiles'
+            # per-lane chains trace them (include/rt_mi355.h rt_stats), so a
+            # split frame may skip more — never fewer, never more than exist
+            assert sr.shadow_rays_moot <= st.shadow_rays_moot <= st.shadow_rays, kw
 
 
 def test_split_sixteenths_of_large_shards_is_invisible(gpu_ctx, rt):

@@ -813,7 +813,10 @@ int refit_update(rt_ctx *ctx, std::chrono::steady_clock::time_point t0) {
 #else
         constexpr float limit = kRefitRebuild;
 #endif
-        if (!(area <= limit * R.area_built)) {
+        // a NaN quality (a degenerate or non-finite scene box: scene_xform.hip
+        // quality_scale) keeps the tree — the refit stays exact, only a
+        // measure of its speed is missing (it rebuilt every update)
+        if (area > limit * R.area_built) {
             std::vector<rtd::MeshGate> aabbs((size_t)ctx->src.mesh_count);
             if (!aabbs.empty())
                 HIP_WAIT(ctx, hipMemcpy(aabbs.data(), ctx->lb.src_aabbs.p, sizeof(rtd::MeshGate) * aabbs.size(),

@@ -405,9 +405,22 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
             __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
             int *cp = F.split_count + sidx * (kWaveSize / 4) + (lane2 >> 2);
+#ifdef RT_EXP_RELACQ
+            // measuring builds: the C++ memory model's release / acquire pair
+            if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == 3) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else
+            // The samples are agent-scope (write-through) stores; waiting for
+            // them before the count makes every one of them reach the device's
+            // coherence point before the count does, and the last arrival's
+            // loads are agent-scope too (they read that point), issued only
+            // after its count returned — the hand-off a release / acquire pair
+            // would give, without the L2 write-back an agent-scope release
+            // costs on gfx950 (A/B: RT_EXP_RELACQ).
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
             if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
+#endif
                 const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (lane2 & ~3)) * 4;
                 auto ld = [](const float *q) {
                     return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
