@@ -265,6 +265,11 @@ struct FrameDev {
     int s16_shift;
     float *split_samples;
     int *split_count;
+    // measuring builds only (RT_EXP_PERSIST): a whole frame's non-split launch
+    // as persist_waves resident waves pulling longest-first tiles from eight
+    // per-XCD tile counters (persist_ctr, 16 ints apart, zeroed per launch)
+    int persist_waves;
+    int *persist_ctr;
 };
 
 }  // namespace rtd

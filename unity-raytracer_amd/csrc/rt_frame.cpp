@@ -525,6 +525,17 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         if (++ctx->count_tag == 0) ++ctx->count_tag;
         F.count_tag = ctx->count_tag;
     }
+#ifdef RT_EXP_PERSIST
+    // measuring builds: whole frames' non-split launches as resident waves
+    if (!count && !levels && F.split_tiles == 0 && F.split16_tiles == 0 && F.num_tiles > kSplit16MaxTiles) {
+        HIP_OR_FAIL(ctx, ensure(ctx, ls->persist_ctr, 8 * 16 * sizeof(int)));
+        HIP_OR_FAIL(ctx, hipMemsetAsync(ls->persist_ctr.p, 0, 8 * 16 * sizeof(int), ctx->stream));
+        F.persist_ctr = (int *)ls->persist_ctr.p;
+        int cus = 0;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+        F.persist_waves = (cus > 0 ? cus : 256) * 4 * RT_EXP_PERSIST;  // RT_EXP_PERSIST waves per SIMD
+    }
+#endif
     // measuring builds (rt_debug_set RT_DEBUG_WAVE_CLOCKS): the launch's per-wave clocks
     if (rtk::kWaveClockBuild && ctx->debug_wave_clock && !count && !levels) {
         const size_t bytes = (size_t)rtk::render_mega_waves(F) * sizeof(uint4);

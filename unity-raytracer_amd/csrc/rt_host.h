@@ -79,6 +79,7 @@ struct LptSlot {
     GrowBuf wave_counts;  // render_kernel's per-wave ray tallies (rtd::FrameDev::wave_counts)
     GrowBuf hints;        // render_kernel's shadow-packet occluder hints (rtd::FrameDev::shadow_hint)
     GrowBuf split_samples, split_count;  // one-sample split waves' hand-off (rtd::FrameDev::split_*)
+    GrowBuf persist_ctr;                 // measuring builds (RT_EXP_PERSIST): per-XCD tile counters
     unsigned long long hints_scene = ~0ull;  // the scene version and layout the hints were recorded for
     long long hints_key = -1;
     long long key = -1;
@@ -87,7 +88,7 @@ struct LptSlot {
     long long frames = 0;
     void release() {
         for (GrowBuf *b : {&cost, &cost_sorted, &iota, &order, &scratch, &wave_counts, &hints, &split_samples,
-                           &split_count}) {
+                           &split_count, &persist_ctr}) {
             if (b->p) (void)hipFree(b->p);
             b->p = nullptr;
             b->cap = 0;

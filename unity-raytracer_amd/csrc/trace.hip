@@ -464,6 +464,44 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     const rtt::Stack st{stack_mem + wave * SS * kWaveSize, ovf, SS};  // + lane per query (traverse)
     int *const wstack = wstack_mem + wave * rtp::kWaveStack;
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+#ifdef RT_EXP_PERSIST
+    // measuring builds: persistent waves over a whole frame's non-split
+    // launch — resident waves take longest-first tile positions p = 8 k + x
+    // from their XCD's counter (x = blockIdx % 8, the dispatch's XCD), until
+    // the frame's tiles are used up; tallies and costs as below
+    if (!COUNT && !SPLIT && F.persist_waves > 0) {
+        const int x = blockIdx.x & 7;
+        int *const ctr = F.persist_ctr + x * 16;
+        if (!F.wave_counts && blockIdx.x == 0 && lane == 0) atomicAdd(rtt::counter_slot(F.counters), F.primary_total);
+        SegClock sg = {0ull, 0ull, 0ull, 0ull};
+        for (;;) {
+            int k = 0;
+            if (rtt::lane_id() == 0) k = atomicAdd(ctr, 1);
+            const int pos = __builtin_amdgcn_readfirstlane(k) * 8 + x;
+            if (pos >= F.num_tiles) break;  // wave-uniform
+            int tile = pos;
+            if (F.tile_order) tile = rtt::cload(F.tile_order + pos);
+            tile = __builtin_amdgcn_readfirstlane(tile);
+            const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
+            const bool sky = render_tile<COUNT, DEEP, Q4, false, false>(S, F, st, wstack, tile, -1, 4,
+                                                                          rtt::lane_id(), cnt, sg, pos);
+            if (F.tile_cost && rtt::lane_id() == 0)
+                F.tile_cost[tile] = sky ? 0u : max(1u, tile_cost_key(__builtin_amdgcn_s_memtime() - t0, -1, 4));
+        }
+        if (F.wave_counts) {
+            unsigned sh = 0, rf = 0, mo = 0;
+            if (__ballot((cnt.shadow | cnt.reflection | cnt.moot) != 0) != 0) {
+                sh = rtt::wave_sum(cnt.shadow);
+                rf = rtt::wave_sum(cnt.reflection);
+                mo = rtt::wave_sum(cnt.moot);
+            }
+            if (rtt::lane_id() == 0) F.wave_counts[blockIdx.x] = make_uint4(sh, rf, mo, F.count_tag);
+        } else {
+            rtt::flush_counts<COUNT>(cnt, F.counters);
+        }
+        return;
+    }
+#endif
     const int wid = blockIdx.x * kMkWaves + wave;
     const int split16 = SPLIT ? F.split16_tiles : 0;
     const int split = SPLIT ? F.split_tiles : 0;
@@ -881,6 +919,13 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     F.primary_total = active_samples(F.res_x, F.res_y, F.local_rows, F.row0, F.band_index, F.band_count, F.band_rows,
                                      F.spp);
     int blocks = (render_mega_waves(F) + kMkWaves - 1) / kMkWaves;
+#ifdef RT_EXP_PERSIST
+    if (F.persist_waves > 0 && !count_tests && F.split_tiles == 0 && F.split16_tiles == 0 && F.max_bounces <= kMaxBounces &&
+        !(S.bvh4 && F.spp >= kLevelsMinSpp))
+        blocks = std::min(blocks, F.persist_waves);
+    else
+        F.persist_waves = 0;
+#endif
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
     const bool shard = F.num_tiles <= kShardTiles;  // a small frame: its slowest waves set its time
     const bool split = F.split_tiles > 0 || F.split16_tiles > 0;
