@@ -323,6 +323,19 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             if (gate >= 0) wgate = -2;  // the lanes' caches moved on their own
         }
     };
+#ifdef RT_EXP_PREFETCH
+    // measuring builds: the internal children a packet will visit later (the
+    // pushed ones) are pulled into L2 right away by LDS-DMA loads whose data
+    // nobody reads (lanes 0..2, one 4-B word of each node line into a dump
+    // area), so their scalar fetch at the pop hits L2
+    __shared__ int pf_dump[rtd::kWaveSize];
+    auto prefetch3 = [&](int a, int b, int c) {
+        const int ln = rtt::lane_id();
+        const int v = ln == 0 ? a : ln == 1 ? b : c;
+        if (ln < 3 && v > 0)
+            __builtin_amdgcn_global_load_lds((const void *)(S.nodes4 + v), (__attribute__((address_space(3))) void *)pf_dump, 4, 0, 0);
+    };
+#endif
     // any-hit: the leaf that retires the most lanes (the next frame's hint)
     int best_leaf = 0, best_retired = 0;  // wave-uniform
     int skip = 0;                         // the hinted leaf, never visited again
@@ -405,6 +418,11 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                 if (n2) { if (nn) RT_PK_PUSH(nxt); nxt = ch.z; ++nn; }
                 if (n1) { if (nn) RT_PK_PUSH(nxt); nxt = ch.y; ++nn; }
                 if (n0) { if (nn) RT_PK_PUSH(nxt); nxt = ch.x; ++nn; }
+#ifdef RT_EXP_PREFETCH
+                if (nn > 1)  // the pushed ones (not the next node: its fetch follows at once)
+                    prefetch3(n3 && nxt != ch.w ? ch.w : -1, n2 && nxt != ch.z ? ch.z : -1,
+                              n1 && nxt != ch.y ? ch.y : -1);
+#endif
                 if (nn) {
                     node = uni(nxt);
                     continue;
@@ -441,6 +459,10 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                 if (q3 != kKeyNone) RT_PK_PUSH(c3);
                 if (q2 != kKeyNone) RT_PK_PUSH(c2);
                 if (q1 != kKeyNone) RT_PK_PUSH(c1);
+#ifdef RT_EXP_PREFETCH
+                if (q1 != kKeyNone)
+                    prefetch3(q3 != kKeyNone ? c3 : -1, q2 != kKeyNone ? c2 : -1, c1);
+#endif
                 node = uni(c0);
                 continue;
             }
