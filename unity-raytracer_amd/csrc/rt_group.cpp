@@ -129,7 +129,15 @@ void release_group(rt_ctx *ctx) {
     for (GroupSlot &g : ctx->gslots) {
         if (!g.used) continue;
         for (int i = 0; i < n && i < (int)g.member_stream.size(); ++i) {
-            (void)hipSetDevice(member(ctx, i)->device);
+            rt_ctx *m = member(ctx, i);
+            (void)hipSetDevice(m->device);
+            // a member's frames ran on this stream (group_frame), and it is
+            // still the member's current stream: back to its own before the
+            // stream is destroyed — destroy_one synchronises the current
+            // stream, and was handed this one's dangling handle until round 5
+            // (whose one caught stall, r05c, had the host inside rt_destroy
+            // of an 8-member group)
+            if (m->stream == g.member_stream[(size_t)i]) m->stream = m->own_stream;
             if (g.member_stream[(size_t)i]) {
                 {
                     const Wait w("destroy: hipStreamSynchronize (a group band stream)");
