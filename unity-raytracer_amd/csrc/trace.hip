@@ -953,7 +953,11 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         RT_LAUNCH((render_kernel<false, true>), "render_kernel<false, true, false, false, 6>");
     else if (S.bvh4 && F.spp >= kLevelsMinSpp) {
         const hipError_t e = launch_render_levels(S, F, stream);
-        name = F.spp <= 16 ? "render_levels_kernel<6>" : "render_levels_kernel<8>";
+        static const char *const lv[2][3] = {{"render_levels_kernel<6, 8>", "render_levels_kernel<6, 16>",
+                                              "render_levels_kernel<6, 32>"},
+                                             {"render_levels_kernel<8, 8>", "render_levels_kernel<8, 16>",
+                                              "render_levels_kernel<8, 32>"}};
+        name = lv[F.spp <= 16 ? 0 : 1][F.max_bounces <= 8 ? 0 : F.max_bounces <= 16 ? 1 : 2];
         if (e != hipSuccess || !F.wave_counts) return e;
         const int waves = F.num_tiles;  // one wave per tile, no splits
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,

@@ -81,7 +81,11 @@ constexpr int kLvStashHigh = 15;
 #define RT_LSEG(...)
 #endif
 
-template <int MIN_WAVES>
+// FD: mirror levels the fold stack holds, the frame's MaxReflectionBounces
+// rounded up to 8, 16 or 32 (launch_render_levels; deeper frames take the
+// megakernel's deep-chain instance): the private segment a wave slot
+// reserves shrinks with it (C4, depth 8: 832 -> 256 B per lane).
+template <int MIN_WAVES, int FD = kMaxBounces>
 __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
     constexpr int STASH = MIN_WAVES == kLvWavesLowSpp ? 18 : kLvStashHigh;  // floats per lane
@@ -104,8 +108,9 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     RT_LSEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
             unsigned long long sg_cam = 0, sg_sh = 0, sg_mir = 0, sg_setup = 0;)
-    float fold_c[kMaxBounces][3];
-    float fold_k[kMaxBounces][3];
+    static_assert(FD <= kMaxBounces, "the frame's depth bucket");
+    float fold_c[FD][3];
+    float fold_k[FD][3];
     int depth = 0;
     f3 term = mk(0.0f, 0.0f, 0.0f);
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
@@ -269,10 +274,25 @@ hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F, hipStream_
     const long long zs = rows * F.tiles_x, ns = (F.num_tiles + zs - 1) / zs;
     const long long grid = 8 * ((ns + 7) / 8) * zs;
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
-    if (F.spp <= 16)
-        hipLaunchKernelGGL(render_levels_kernel<kLvWavesLowSpp>, dim3((unsigned)grid), dim3(kWaveSize), 0, stream, S, F);
-    else
-        hipLaunchKernelGGL(render_levels_kernel<kLvWavesHighSpp>, dim3((unsigned)grid), dim3(kWaveSize), 0, stream, S, F);
+    const dim3 g((unsigned)grid), b(kWaveSize);
+    // the fold stack's depth bucket (render_levels_kernel FD); frames deeper
+    // than kMaxBounces never come here (rt_frame.cpp frame_path)
+    const int fd = F.max_bounces <= 8 ? 8 : F.max_bounces <= 16 ? 16 : kMaxBounces;
+    if (F.spp <= 16) {
+        if (fd == 8)
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, 8>), g, b, 0, stream, S, F);
+        else if (fd == 16)
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, 16>), g, b, 0, stream, S, F);
+        else
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, kMaxBounces>), g, b, 0, stream, S, F);
+    } else {
+        if (fd == 8)
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, 8>), g, b, 0, stream, S, F);
+        else if (fd == 16)
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, 16>), g, b, 0, stream, S, F);
+        else
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, kMaxBounces>), g, b, 0, stream, S, F);
+    }
     return hipGetLastError();
 }
 
