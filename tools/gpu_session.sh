@@ -63,8 +63,11 @@ if has bench; then
 fi
 if has kt; then
   cd /tmp
+  # the bench's timed frames (no moving camera: the in-flight instance's last 50 launches are the timed
+  # frames; tools/kt_span.py --last 50 gives their device time per launch, bench.py's roofline.avg_kernel_ms)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/kt_$tag -o run --output-format csv -- \
-    python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/$out/kt_$tag.log 2>&1 || fail kt $R/$out/kt_$tag.log
+    python3 $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline --moving-frames 0 > $R/$out/kt_$tag.log 2>&1 \
+    || fail kt $R/$out/kt_$tag.log
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/kts1_$tag -o run --output-format csv -- \
     python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --streams 1 --moving-frames 0 \
     > $R/$out/kts1_$tag.log 2>&1 || fail kts1 $R/$out/kts1_$tag.log

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("trace_dir")
     ap.add_argument("--kernel", default="")
     ap.add_argument("--min-grid", type=int, default=0, help="ignore dispatches with a smaller grid (warm-up frames)")
+    ap.add_argument("--last", type=int, default=0,
+                    help="only the last N full-grid dispatches (bench.py --moving-frames 0: its timed frames are the "
+                         "last launches of the in-flight instance)")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True)
     if not files:
@@ -43,6 +46,8 @@ def main():
     for name, lst in sorted(iv.items(), key=lambda kv: -sum(e - s for s, e, _ in kv[1])):
         big = max(g for _, _, g in lst)
         lst = sorted((s, e) for s, e, g in lst if g == big)  # the workload's launches, not warm-up frames
+        if a.last:
+            lst = lst[-a.last:]
         durs = [(e - s) * 1e-6 for s, e in lst]
         union, cur_s, cur_e = 0, None, None
         for s, e in lst:
