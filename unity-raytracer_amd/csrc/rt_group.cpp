@@ -73,8 +73,11 @@ void destroy_one(rt_ctx *ctx) {
         ctx->copier.stop();
     }
     {
-        const Wait w("destroy: hipStreamSynchronize (stream, copy stream, slab stream)");
-        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        // only the context's own streams: its current stream may be a caller's
+        // (rt_set_stream) that no longer exists — the frees below wait for
+        // the device anyway
+        const Wait w("destroy: hipStreamSynchronize (own, copy and slab streams)");
+        if (ctx->own_stream) (void)hipStreamSynchronize(ctx->own_stream);
         if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
         if (ctx->slab_stream2) (void)hipStreamSynchronize(ctx->slab_stream2);
     }
