@@ -14,6 +14,7 @@
 #   cfg      C4 / C5 bench lines (whole frame and 1/8 share)
 #   abx      interleaved A/B: AB_VARIANTS (default "base,default") on C3, C2, C4, C5 and C3 shares
 #   e2e      rt_render end to end (RGBA8 and float)
+#   e2etr    rt_render timelines: rocprofv3 runtime/marker/kernel/copy traces, tools/e2e_trace.py
 #   wclk     per-wave clocks (needs lib/variants/wclk)
 #   parity   full-size whole-frame oracle parity (tests -m fullsize)
 # Output under gpurun_out/ (<stage>_<tag>.log); copy what is judged to profiles/.
@@ -122,6 +123,19 @@ if has e2e; then
       || fail e2e $out/e2e_$tag.log
   done
   echo e2e-ok
+fi
+if has e2etr; then
+  # rt_render timelines (runtime + marker + kernel + copy traces; no counters)
+  cd /tmp
+  for fl in 8 0; do
+    timeout -k 10 200 rocprofv3 --runtime-trace --marker-trace --kernel-trace --memory-copy-trace --output-format csv \
+      -d $R/$out/e2etr_${fl}_$tag -o run -- python3 $R/tools/e2e_trace.py run --flags $fl --frames 12 \
+      > $R/$out/e2etr_${fl}_$tag.log 2>&1 || fail e2etr-$fl $R/$out/e2etr_${fl}_$tag.log
+  done
+  cd $R
+  for fl in 8 0; do python3 tools/e2e_trace.py analyse $out/e2etr_${fl}_$tag --flags $fl; done > $out/e2etr_$tag.jsonl \
+    || fail e2etr-analyse $out/e2etr_$tag.jsonl
+  echo e2etr-ok
 fi
 if has wclk; then
   timeout -k 10 300 python tools/wave_clock.py --config C3 --bands 1,2,4,8 > $out/wclk_$tag.log 2>&1 \
