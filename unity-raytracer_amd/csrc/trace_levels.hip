@@ -222,7 +222,39 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         term = mk(fold_c[k][0], fold_c[k][1], fold_c[k][2]) + mk(fold_k[k][0], fold_k[k][1], fold_k[k][2]) * term;
     // lane ids recomputed (rtt::lane_id), not kept live across the levels
     const int lane2 = rtt::lane_id();
+#ifdef RT_EXP_LDSSUM
+    // measuring builds: the samples go to LDS (the stash area, free here) in
+    // one write per lane; each pixel's sample-0 lane then reads its pixel's
+    // samples back 4 floats at a time and adds them in sample order — the
+    // same sums, with spp / 4 * 3 narrow reads instead of (spp - 1) * 3
+    // whole-wave lane shuffles
+    f3 sum = term;
+    if (F.spp >= 16) {
+        float *sm = stash_mem;
+        sm[lane2 * 3 + 0] = term.x;
+        sm[lane2 * 3 + 1] = term.y;
+        sm[lane2 * 3 + 2] = term.z;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if ((lane2 & (F.spp - 1)) == 0) {
+            // 4 samples = 12 floats = 3 aligned float4 per step
+            const float4 *q = reinterpret_cast<const float4 *>(sm + lane2 * 3);
+            for (int k = 0; k < F.spp; k += 4) {
+                const float4 a = q[0], b = q[1], c = q[2];
+                q += 3;
+                sum = k == 0 ? mk(a.x, a.y, a.z) : sum + mk(a.x, a.y, a.z);
+                sum = sum + mk(a.w, b.x, b.y);
+                sum = sum + mk(b.z, b.w, c.x);
+                sum = sum + mk(c.y, c.z, c.w);
+            }
+        }
+    } else {
+        sum = rts::sample_sum(term, lane2, F.spp);
+    }
+#else
     const f3 sum = rts::sample_sum(term, lane2, F.spp);
+#endif
     {
         int tile2 = __builtin_amdgcn_readfirstlane(tile);
         asm volatile("" : "+s"(tile2));
