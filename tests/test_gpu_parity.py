@@ -56,7 +56,9 @@ def test_frame_vs_oracle(gpu_ctx, rt, orc, name, res, spp, mode):
     _check(img, ref, st, counts, f"{name}/{mode}")
 
 
-@pytest.mark.parametrize("name,res,spp", [("C3", (48, 27), 16), ("C2", (40, 24), 64), ("C5", (24, 14), 16)])
+@pytest.mark.parametrize("name,res,spp", [("C3", (48, 27), 16), ("C2", (40, 24), 64), ("C5", (24, 14), 16),
+                                          ("C3", (26, 15), 25), ("C2", (22, 13), 36), ("C5", (14, 9), 49),
+                                          ("C3", (20, 11), 64)])
 def test_levels_kernel_vs_oracle(gpu_ctx, rt, orc, name, res, spp):
     """>= 16 spp frames take the level-synchronous all-packet megakernel
     (render_levels_kernel): whole frames against the oracle, mirror chains
