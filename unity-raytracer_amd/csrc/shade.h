@@ -123,16 +123,31 @@ __device__ __forceinline__ void reflect(const Surface &s, f3 &o, f3 &d) {
     d = ((2.0f * s.n) * rtm::dot(s.view, s.n)) - s.view;
 }
 
+// A frame shape fixed at compile time (FIX = n, the samples per pixel edge):
+// 0 reads it from F (any n x n spp); 2: 2x2 spp in 4x4-pixel tiles (Q4, the
+// bench configurations); 4: 4x4 spp in 2x2-pixel tiles and 8: 8x8 spp in
+// one-pixel tiles (the levels kernel's 16 and 64 spp).  The lane -> sample
+// and pixel splits are then shifts and masks, and (i + 0.5) / n is an exact
+// scaling by a power of two (the same value as the division).  The tile
+// sizes are prepare_frame's (rt_frame.cpp): 64 / spp pixels per wave as a
+// near-square 2^a x 2^b block.
+template <int FIX>
+struct Fix {
+    static_assert(FIX == 0 || FIX == 2 || FIX == 4 || FIX == 8, "fixed frame shapes");
+    static constexpr int lg_n = FIX == 2 ? 1 : FIX == 4 ? 2 : FIX == 8 ? 3 : 0;
+    static constexpr int tw = FIX == 2 ? 4 : FIX == 4 ? 2 : 1;  // tile edge in pixels
+    static constexpr int lg_tw = FIX == 2 ? 2 : FIX == 4 ? 1 : 0;
+};
+
 // Primary ray of sample (px, gy, sub-sample s): CastPixelRays :291-298 with
 // n*n stratified offsets ((i + 0.5) / n; n == 1 gives the reference's 0.5).
-// Q4: the frame is 2x2 spp in 4x4-pixel tiles (the bench configurations):
-// the lane -> sample split is shifts, and (i + 0.5) / 2 is an exact halving.
-template <bool Q4 = false>
+template <int FIX = 0>
 __device__ __forceinline__ void primary_ray(const rtd::FrameDev &F, int px, int gy, int s, f3 &o, f3 &d) {
-    const int n = Q4 ? 2 : F.spp_n;
-    const int sj = Q4 ? s >> 1 : s / n, si = Q4 ? s & 1 : s - sj * n;
-    const float ox = Q4 ? ((float)si + 0.5f) * 0.5f : ((float)si + 0.5f) / (float)n;
-    const float oy = Q4 ? ((float)sj + 0.5f) * 0.5f : ((float)sj + 0.5f) / (float)n;
+    using X = Fix<FIX>;
+    const int n = FIX ? FIX : F.spp_n;
+    const int sj = FIX ? s >> X::lg_n : s / n, si = FIX ? s & (FIX - 1) : s - sj * n;
+    const float ox = FIX ? ((float)si + 0.5f) * (1.0f / (float)FIX) : ((float)si + 0.5f) / (float)n;
+    const float oy = FIX ? ((float)sj + 0.5f) * (1.0f / (float)FIX) : ((float)sj + 0.5f) / (float)n;
     const float rm = (((float)px + ox) * F.hl) / (float)F.res_x;
     const float dm = (((float)gy + oy) * F.vl) / (float)F.res_y;
     const f3 pp = (rtt::ld3(F.top_left) + rm * rtt::ld3(F.right)) - rtt::ld3(F.up) * dm;
@@ -145,11 +160,12 @@ __device__ __forceinline__ void primary_ray(const rtd::FrameDev &F, int px, int 
 // reciprocals (relative error ~1e-6, far inside the pad), surely misses the
 // padded Scene.AABB — then the exact ray misses the exact gate (Scene.cs:54).
 // A NaN anywhere leaves the answer "maybe" (fminf/fmaxf ignore NaN operands).
-template <bool Q4 = false>
+template <int FIX = 0>
 __device__ __forceinline__ bool sky_maybe(const rtd::FrameDev &F, int px, int gy, int s) {
-    const int n = Q4 ? 2 : F.spp_n;
-    const int sj = Q4 ? s >> 1 : s / n, si = Q4 ? s & 1 : s - sj * n;
-    const float rn = Q4 ? 0.5f : __builtin_amdgcn_rcpf((float)n);
+    using X = Fix<FIX>;
+    const int n = FIX ? FIX : F.spp_n;
+    const int sj = FIX ? s >> X::lg_n : s / n, si = FIX ? s & (FIX - 1) : s - sj * n;
+    const float rn = FIX ? 1.0f / (float)FIX : __builtin_amdgcn_rcpf((float)n);
     const float ax = ((float)px + ((float)si + 0.5f) * rn) * F.sky_hx;
     const float ay = ((float)gy + ((float)sj + 0.5f) * rn) * F.sky_vy;
     const float dx = F.sky_tlc[0] + ax * F.right[0] - ay * F.up[0];
@@ -236,9 +252,9 @@ __device__ __forceinline__ void tile_xy(const rtd::FrameDev &F, int tile, int &t
 // The pixel rectangle of a tile (image rows; tile index wave-uniform) for the
 // camera packet's frustum start (packet.h cut_start).  Valid when a tile's
 // rows lie in one band block (rt_abi.cpp cut_setup checks band_rows).
-template <bool Q4 = false>
+template <int FIX = 0>
 __device__ __forceinline__ rtp::TileRect tile_rect(const rtd::FrameDev &F, int tile) {
-    const int tw = Q4 ? 4 : F.tile_w, th = Q4 ? 4 : F.tile_h;
+    const int tw = FIX ? Fix<FIX>::tw : F.tile_w, th = FIX ? Fix<FIX>::tw : F.tile_h;
     int tx, ty;
     tile_xy(F, tile, tx, ty);
     const int ly = ty * th;
@@ -252,18 +268,19 @@ __device__ __forceinline__ rtp::TileRect tile_rect(const rtd::FrameDev &F, int t
 
 // Slot (tile, lane) -> pixel; false for lanes outside the image/shard.  A
 // pixel's samples sit in consecutive lanes.
-template <bool Q4 = false>
+template <int FIX = 0>
 __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int lane, int &px, int &ly, int &gy,
                                            int &s) {
-    const int spp = Q4 ? 4 : F.spp;
-    const int lp = Q4 ? lane >> 2 : lane / spp;
+    using X = Fix<FIX>;
+    const int spp = FIX ? FIX * FIX : F.spp;
+    const int lp = FIX ? lane >> (2 * X::lg_n) : lane / spp;
     const int pix = lp;
-    s = Q4 ? lane & 3 : lane - lp * spp;
-    const int tw = Q4 ? 4 : F.tile_w, th = Q4 ? 4 : F.tile_h;
+    s = FIX ? lane & (FIX * FIX - 1) : lane - lp * spp;
+    const int tw = FIX ? X::tw : F.tile_w, th = FIX ? X::tw : F.tile_h;
     int tx, ty;
     tile_xy(F, tile, tx, ty);
-    px = tx * tw + (Q4 ? pix & 3 : pix % tw);
-    ly = ty * th + (Q4 ? pix >> 2 : pix / tw);
+    px = tx * tw + (FIX ? pix & (X::tw - 1) : pix % tw);
+    ly = ty * th + (FIX ? pix >> X::lg_tw : pix / tw);
     gy = ly + F.row0;
     if (F.band_count > 1) {
         const int blk = ly / F.band_rows;

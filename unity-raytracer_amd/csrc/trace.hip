@@ -353,29 +353,29 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     int px, ly, gy, s;
 #ifdef RT_EXP_ONESAMPLE
     // measuring builds only (wrong images): a sixteenth-wave traces its pixel's first sample alone
-    const bool active = rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) &&
+    const bool active = rts::slot_pixel<Q4 ? 2 : 0>(F, tile, lane, px, ly, gy, s) &&
                         (part < 0 || ((lane >> pshift) == part && (pshift != 2 || (lane & 3) == RT_EXP_ONESAMPLE)));
 #else
     const bool active =
-        rts::slot_pixel<Q4>(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
+        rts::slot_pixel<Q4 ? 2 : 0>(F, tile, lane, px, ly, gy, s) && (part < 0 || (lane >> pshift) == part);
 #endif
     f3 color = mk(0.0f, 0.0f, 0.0f);
     // a wave whose samples all surely miss the padded Scene.AABB is background
     // without its exact rays (shade.h sky_maybe; the counting launch traces all)
     bool sky = false;
 #ifndef RT_EXP_NOSKY
-    if (!COUNT) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4>(F, px, gy, s))) == 0;
+    if (!COUNT) sky = __ballot(active && (!F.sky_test || rts::sky_maybe<Q4 ? 2 : 0>(F, px, gy, s))) == 0;
 #endif
     // the camera packet's start below the top-level cut (every lane active here)
     rtp::CutStart cs = {0, 0, 0, -1};
-    if (!COUNT && !sky && F.cut_test) cs = rtp::cut_select(S, F, rts::tile_rect<Q4>(F, tile), wstack, &cl);
+    if (!COUNT && !sky && F.cut_test) cs = rtp::cut_select(S, F, rts::tile_rect<Q4 ? 2 : 0>(F, tile), wstack, &cl);
     if (active) {
         if (COUNT) cnt.primary += 1;  // otherwise F.primary_total, added once per launch
         if (sky) {
             color = rtt::ld3(F.bg255);  // :310-311
         } else {
             f3 o, d;
-            rts::primary_ray<Q4>(F, px, gy, s, o, d);
+            rts::primary_ray<Q4 ? 2 : 0>(F, px, gy, s, o, d);
             if (COUNT) {  // trivially cheap camera samples: they miss Scene.AABB (Scene.cs:54)
                 rtt::RayCtx rg;
                 rtt::setup_ray(rg, o, d);
@@ -393,7 +393,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     asm volatile("" : "+s"(tile2));
     const int lane2 = rtt::lane_id();
     const bool active2 =
-        rts::slot_pixel<Q4>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
+        rts::slot_pixel<Q4 ? 2 : 0>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
     if (HINT && !COUNT && pshift == 0 && (Q4 || F.spp == 4)) {
         // a one-sample wave of a split pixel: its sample goes to the pixel's
         // slots by write-through (sc1) stores, then the pixel's arrival count;
@@ -953,11 +953,12 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         RT_LAUNCH((render_kernel<false, true>), "render_kernel<false, true, false, false, 6>");
     else if (S.bvh4 && F.spp >= kLevelsMinSpp) {
         const hipError_t e = launch_render_levels(S, F, stream);
-        static const char *const lv[2][3] = {{"render_levels_kernel<6, 8>", "render_levels_kernel<6, 16>",
-                                              "render_levels_kernel<6, 32>"},
-                                             {"render_levels_kernel<8, 8>", "render_levels_kernel<8, 16>",
-                                              "render_levels_kernel<8, 32>"}};
-        name = lv[F.spp <= 16 ? 0 : 1][F.max_bounces <= 8 ? 0 : F.max_bounces <= 16 ? 1 : 2];
+        static const char *const lv[2][3] = {{"render_levels_kernel<6, 8, 4>", "render_levels_kernel<6, 16, 4>",
+                                              "render_levels_kernel<6, 32, 4>"},
+                                             {"render_levels_kernel<8, 8, 8>", "render_levels_kernel<8, 16, 8>",
+                                              "render_levels_kernel<8, 32, 8>"}};
+        name = F.spp > 16 && F.spp != 64 ? "render_levels_kernel<8, 32, 0>"
+                                         : lv[F.spp <= 16 ? 0 : 1][F.max_bounces <= 8 ? 0 : F.max_bounces <= 16 ? 1 : 2];
         if (e != hipSuccess || !F.wave_counts) return e;
         const int waves = F.num_tiles;  // one wave per tile, no splits
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,

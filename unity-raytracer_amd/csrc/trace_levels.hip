@@ -85,7 +85,12 @@ constexpr int kLvStashHigh = 15;
 // rounded up to 8, 16 or 32 (launch_render_levels; deeper frames take the
 // megakernel's deep-chain instance): the private segment a wave slot
 // reserves shrinks with it (C4, depth 8: 832 -> 256 B per lane).
-template <int MIN_WAVES, int FD = kMaxBounces>
+// FIX: the frame shape fixed at compile time (shade.h rts::Fix): 4 for 16
+// spp (2x2-pixel tiles), 8 for 64 spp (one-pixel tiles), 0 for 25 / 36 / 49
+// spp — the slot -> sample mapping and the sub-pixel offsets by shifts
+// instead of integer and float divisions (C4's per-wave setup was 30 % of
+// its wave, seglv_r05h).
+template <int MIN_WAVES, int FD = kMaxBounces, int FIX = 0>
 __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
     constexpr int STASH = MIN_WAVES == kLvWavesLowSpp ? 18 : kLvStashHigh;  // floats per lane
@@ -117,18 +122,18 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     bool alive;
     {
         int px, ly, gy, s;
-        alive = rts::slot_pixel(F, tile, lane, px, ly, gy, s);
+        alive = rts::slot_pixel<FIX>(F, tile, lane, px, ly, gy, s);
         // a wave whose samples all surely miss the padded Scene.AABB is
         // background without its exact rays (shade.h sky_maybe, as render_kernel)
         // (the <= 16-spp instance: C4 -8 %; at 64 spp, 1-pixel tiles, +1 %)
         const bool sky = MIN_WAVES == kLvWavesLowSpp &&
-                         __ballot(alive && (!F.sky_test || rts::sky_maybe(F, px, gy, s))) == 0;
+                         __ballot(alive && (!F.sky_test || rts::sky_maybe<FIX>(F, px, gy, s))) == 0;
         if (alive) {
             if (!F.wave_counts) cnt.primary = 1;  // otherwise F.primary_total, once per launch
             if (sky)
                 term = rtt::ld3(F.bg255);  // :310-311
             else
-                rts::primary_ray(F, px, gy, s, o, d);
+                rts::primary_ray<FIX>(F, px, gy, s, o, d);
         }
         if (sky) alive = false;
     }
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     rtp::CutStart cs = {0, 0, 0, -1};
     if (CUT && F.cut_test && __ballot(alive) != 0) {  // every lane executes here
         const rtp::CutLane cl = rtp::cut_load(S);
-        cs = rtp::cut_select(S, F, rts::tile_rect(F, tile), wstack_mem, &cl);
+        cs = rtp::cut_select(S, F, rts::tile_rect<FIX>(F, tile), wstack_mem, &cl);
     }
     RT_LSEG(sg_setup = __builtin_amdgcn_s_memtime() - ts0;)
     for (int level = 0; __ballot(alive) != 0; ++level) {  // wave-uniform
@@ -230,8 +235,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     // shuffles with a small fraction of their LDS traffic: C5 (64 spp)
     // -7.8 %, C4 (16 spp) -3.2 %, bit-identical (r05g).
     f3 sum = term;
-    if ((F.spp & (F.spp - 1)) == 0) {  // wave-uniform: 16 or 64 spp (sample-0 lanes 16-aligned);
-        // 25 / 36 / 49 spp (pixels at lane offsets that are no multiple of 4) take the shuffles
+    if (FIX != 0) {  // 16 or 64 spp (sample-0 lanes 16-aligned); 25 / 36 / 49 spp take the shuffles
         float *sm = stash_mem;
         sm[lane2 * 3 + 0] = term.x;
         sm[lane2 * 3 + 1] = term.y;
@@ -239,9 +243,10 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if ((lane2 & (F.spp - 1)) == 0) {
+        constexpr int SPP = FIX * FIX;
+        if ((lane2 & (SPP - 1)) == 0) {
             const float4 *q = reinterpret_cast<const float4 *>(sm + lane2 * 3);
-            for (int k = 0; k < F.spp; k += 4) {  // 4 samples = 12 floats
+            for (int k = 0; k < SPP; k += 4) {  // 4 samples = 12 floats
                 const float4 a = q[0], b = q[1], c = q[2];
                 q += 3;
                 sum = k == 0 ? mk(a.x, a.y, a.z) : sum + mk(a.x, a.y, a.z);
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         int tile2 = __builtin_amdgcn_readfirstlane(tile);
         asm volatile("" : "+s"(tile2));
         int px, ly, gy, s;
-        if (rts::slot_pixel(F, tile2, lane2, px, ly, gy, s) && s == 0) {
+        if (rts::slot_pixel<FIX>(F, tile2, lane2, px, ly, gy, s) && s == 0) {
             f3 v = sum;
             if (F.spp > 1) v = (F.spp & (F.spp - 1)) == 0 ? v * F.inv_spp : v / (float)F.spp;
             rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
@@ -308,20 +313,22 @@ hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F, hipStream_
     // the fold stack's depth bucket (render_levels_kernel FD); frames deeper
     // than kMaxBounces never come here (rt_frame.cpp frame_path)
     const int fd = F.max_bounces <= 8 ? 8 : F.max_bounces <= 16 ? 16 : kMaxBounces;
-    if (F.spp <= 16) {
+    if (F.spp <= 16) {  // 16 spp: FIX 4
         if (fd == 8)
-            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, 8>), g, b, 0, stream, S, F);
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, 8, 4>), g, b, 0, stream, S, F);
         else if (fd == 16)
-            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, 16>), g, b, 0, stream, S, F);
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, 16, 4>), g, b, 0, stream, S, F);
         else
-            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, kMaxBounces>), g, b, 0, stream, S, F);
-    } else {
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesLowSpp, kMaxBounces, 4>), g, b, 0, stream, S, F);
+    } else if (F.spp == 64) {
         if (fd == 8)
-            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, 8>), g, b, 0, stream, S, F);
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, 8, 8>), g, b, 0, stream, S, F);
         else if (fd == 16)
-            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, 16>), g, b, 0, stream, S, F);
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, 16, 8>), g, b, 0, stream, S, F);
         else
-            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, kMaxBounces>), g, b, 0, stream, S, F);
+            hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, kMaxBounces, 8>), g, b, 0, stream, S, F);
+    } else {  // 25 / 36 / 49 spp
+        hipLaunchKernelGGL((render_levels_kernel<kLvWavesHighSpp, kMaxBounces, 0>), g, b, 0, stream, S, F);
     }
     return hipGetLastError();
 }
