@@ -219,6 +219,7 @@ struct FrameDev {
     int spp, spp_n;          // samples per pixel = spp_n * spp_n
     int max_bounces;
     int band_index, band_count, band_rows;
+    unsigned band_rows_magic;  // floor(2^32 / band_rows) (0xffffffff for 1): shade.h band_block
     int local_rows;          // rows of the compact output buffer
     int row0;                // band_count == 1: first image row of this launch (a row slab of rt_render)
     int tile_w, tile_h;      // pixels of one wave's tile

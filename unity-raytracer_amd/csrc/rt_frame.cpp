@@ -132,6 +132,7 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.band_index = prm->band_index;
     F.band_count = band_count;
     F.band_rows = band_rows;
+    F.band_rows_magic = band_rows <= 1 ? 0xffffffffu : (unsigned)((1ull << 32) / (unsigned long long)band_rows);
     F.local_rows = band_local_rows(F.res_y, band_count, band_rows);
     // tile: 64/spp pixels per wave; a power of two is laid out as a
     // near-square 2^a x 2^b block

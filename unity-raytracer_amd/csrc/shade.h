@@ -249,6 +249,21 @@ __device__ __forceinline__ void tile_xy(const rtd::FrameDev &F, int tile, int &t
     ty = (int)q;
 }
 
+// Local row -> (band block, row in the block), ly = blk * band_rows + r, by
+// the per-frame magic multiplier (FrameDev::band_rows_magic = floor(2^32 /
+// band_rows)) like tile_xy: exact for every non-negative row, without the
+// integer-division sequence that cost each shard lane two of them per tile.
+__device__ __forceinline__ void band_block(const rtd::FrameDev &F, int ly, int &blk, int &r) {
+    unsigned q = __umulhi((unsigned)ly, F.band_rows_magic);
+    int rr = ly - (int)q * F.band_rows;
+    if (rr >= F.band_rows) {
+        ++q;
+        rr -= F.band_rows;
+    }
+    blk = (int)q;
+    r = rr;
+}
+
 // The pixel rectangle of a tile (image rows; tile index wave-uniform) for the
 // camera packet's frustum start (packet.h cut_start).  Valid when a tile's
 // rows lie in one band block (rt_abi.cpp cut_setup checks band_rows).
@@ -260,8 +275,9 @@ __device__ __forceinline__ rtp::TileRect tile_rect(const rtd::FrameDev &F, int t
     const int ly = ty * th;
     int gy = ly + F.row0;
     if (F.band_count > 1) {
-        const int blk = ly / F.band_rows;
-        gy = (blk * F.band_count + F.band_index) * F.band_rows + (ly - blk * F.band_rows);
+        int blk, r;  // ly = blk * band_rows + r, by the magic multiplier (no division)
+        band_block(F, ly, blk, r);
+        gy = (blk * F.band_count + F.band_index) * F.band_rows + r;
     }
     return rtp::TileRect{tx * tw, gy, tw, th};
 }
@@ -283,8 +299,9 @@ __device__ __forceinline__ bool slot_pixel(const rtd::FrameDev &F, int tile, int
     ly = ty * th + (FIX ? pix >> X::lg_tw : pix / tw);
     gy = ly + F.row0;
     if (F.band_count > 1) {
-        const int blk = ly / F.band_rows;
-        gy = (blk * F.band_count + F.band_index) * F.band_rows + (ly - blk * F.band_rows);
+        int blk, r;  // ly = blk * band_rows + r, by the magic multiplier (no division)
+        band_block(F, ly, blk, r);
+        gy = (blk * F.band_count + F.band_index) * F.band_rows + r;
     }
     return lp < rtd::kWaveSize / spp && pix < tw * th && px < F.res_x && ly < F.local_rows && gy < F.res_y;
 }
