@@ -220,6 +220,8 @@ struct FrameDev {
     int max_bounces;
     int band_index, band_count, band_rows;
     unsigned band_rows_magic;  // floor(2^32 / band_rows) (0xffffffff for 1): shade.h band_block
+    int lv_zs;                 // render_levels_kernel: tiles per XCD stripe, and floor(2^32 / lv_zs)
+    unsigned lv_zs_magic;      // (set by launch_render_levels for the instance it launches)
     int local_rows;          // rows of the compact output buffer
     int row0;                // band_count == 1: first image row of this launch (a row slab of rt_render)
     int tile_w, tile_h;      // pixels of one wave's tile

@@ -104,9 +104,16 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     // order, so each XCD's L2 serves the geometry of one eighth of the screen
     // instead of all of it — C5 -3 %, C4 -2 % with frames in flight (r04g).
     // A frame's tiles are all here exactly once, whatever the placement.
-    const int zs = (MIN_WAVES == kLvWavesLowSpp ? kXcdStripeRowsLow : kXcdStripeRowsHigh) * F.tiles_x;
+    // (k / zs, k % zs by the launcher's magic multiplier: no scalar division)
+    const int zs = F.lv_zs;
     const int k = blockIdx.x >> 3;
-    const int wid = ((k / zs) * 8 + (blockIdx.x & 7)) * zs + k % zs;  // the tile itself
+    unsigned q = __umulhi((unsigned)k, F.lv_zs_magic);
+    int rk = k - (int)q * zs;
+    if (rk >= zs) {
+        ++q;
+        rk -= zs;
+    }
+    const int wid = ((int)q * 8 + (blockIdx.x & 7)) * zs + rk;  // the tile itself
     if (wid >= F.num_tiles) return;  // wave-uniform (the last stripes' padding)
     // the tile index in an SGPR (scalar slot -> pixel math, nothing spilled)
     int tile = __builtin_amdgcn_readfirstlane(wid);
@@ -302,11 +309,14 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
 
 namespace rtk {
 
-hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F, hipStream_t stream) {
-    if (F.num_tiles <= 0) return hipSuccess;
+hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F0, hipStream_t stream) {
+    if (F0.num_tiles <= 0) return hipSuccess;
+    FrameDev F = F0;
     // whole groups of eight stripes (render_levels_kernel's XCD-aware dispatch)
     const long long rows = F.spp <= 16 ? kXcdStripeRowsLow : kXcdStripeRowsHigh;  // the instance launched below
     const long long zs = rows * F.tiles_x, ns = (F.num_tiles + zs - 1) / zs;
+    F.lv_zs = (int)zs;
+    F.lv_zs_magic = zs <= 1 ? 0xffffffffu : (unsigned)((1ull << 32) / (unsigned long long)zs);
     const long long grid = 8 * ((ns + 7) / 8) * zs;
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
     const dim3 g((unsigned)grid), b(kWaveSize);
