@@ -27,7 +27,11 @@ namespace {
 // interleaved A/B): C4 (16 spp, depth 8) 6 waves -5 % single frame / -8 %
 // frames in flight against 7; C5 (64 spp, depth 16) 6 waves +2 %, 5 waves
 // +6 % against 7; 8 waves -1.1 % against 7 (r04l).
+#ifdef RT_EXP_LVLOW
+constexpr int kLvWavesLowSpp = RT_EXP_LVLOW;  // measuring builds only
+#else
 constexpr int kLvWavesLowSpp = 6;
+#endif
 #ifdef RT_EXP_LVHIGH
 constexpr int kLvWavesHighSpp = RT_EXP_LVHIGH;  // measuring builds only
 #else
@@ -93,7 +97,8 @@ constexpr int kLvStashHigh = 15;
 template <int MIN_WAVES, int FD = kMaxBounces, int FIX = 0>
 __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(SceneDev S, FrameDev F) {
     __shared__ int wstack_mem[rtp::kWaveStack];
-    constexpr int STASH = MIN_WAVES == kLvWavesLowSpp ? 18 : kLvStashHigh;  // floats per lane
+    constexpr bool LOW = FIX == 4;  // the 16-spp instance (2x2-pixel tiles)
+    constexpr int STASH = LOW ? 18 : kLvStashHigh;  // floats per lane
     // (volatile: reloaded after the packet, so the register copies die at the store)
     __shared__ float stash_mem[(STASH > 0 ? STASH : 1) * kWaveSize];
     const int lane = threadIdx.x & 63;
@@ -133,7 +138,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         // a wave whose samples all surely miss the padded Scene.AABB is
         // background without its exact rays (shade.h sky_maybe, as render_kernel)
         // (the <= 16-spp instance: C4 -8 %; at 64 spp, 1-pixel tiles, +1 %)
-        const bool sky = MIN_WAVES == kLvWavesLowSpp &&
+        const bool sky = LOW &&
                          __ballot(alive && (!F.sky_test || rts::sky_maybe<FIX>(F, px, gy, s))) == 0;
         if (alive) {
             if (!F.wave_counts) cnt.primary = 1;  // otherwise F.primary_total, once per launch
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     // frames in flight (r04l).  Not at 64 spp: a one-pixel tile's frustum
     // touches most of C5's heavily overlapping top-level boxes, and every
     // waiting entry costs a scalar round trip when popped: C5 +43 %.
-    constexpr bool CUT = MIN_WAVES == kLvWavesLowSpp;
+    constexpr bool CUT = LOW;
     rtp::CutStart cs = {0, 0, 0, -1};
     if (CUT && F.cut_test && __ballot(alive) != 0) {  // every lane executes here
         const rtp::CutLane cl = rtp::cut_load(S);
