@@ -171,8 +171,8 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     if spp >= 16 and not deep:
         fd = 8 if depth <= 8 else 16 if depth <= 16 else 32  # the fold stack's depth bucket
         if spp > 16 and spp != 64:
-            return "render_levels_kernel<8, 32, 0>"
-        return f"render_levels_kernel<{6 if spp <= 16 else 8}, {fd}, {4 if spp <= 16 else 8}>"
+            return "render_levels_kernel<7, 32, 0>"
+        return f"render_levels_kernel<{6 if spp <= 16 else 7}, {fd}, {4 if spp <= 16 else 8}>"
     ppw = 64 // spp
     lg = ppw.bit_length() - 1
     th = 1 << (lg // 2) if ppw & (ppw - 1) == 0 else 1

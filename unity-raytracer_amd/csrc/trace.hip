@@ -955,9 +955,9 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         const hipError_t e = launch_render_levels(S, F, stream);
         static const char *const lv[2][3] = {{"render_levels_kernel<6, 8, 4>", "render_levels_kernel<6, 16, 4>",
                                               "render_levels_kernel<6, 32, 4>"},
-                                             {"render_levels_kernel<8, 8, 8>", "render_levels_kernel<8, 16, 8>",
-                                              "render_levels_kernel<8, 32, 8>"}};
-        name = F.spp > 16 && F.spp != 64 ? "render_levels_kernel<8, 32, 0>"
+                                             {"render_levels_kernel<7, 8, 8>", "render_levels_kernel<7, 16, 8>",
+                                              "render_levels_kernel<7, 32, 8>"}};
+        name = F.spp > 16 && F.spp != 64 ? "render_levels_kernel<7, 32, 0>"
                                          : lv[F.spp <= 16 ? 0 : 1][F.max_bounces <= 8 ? 0 : F.max_bounces <= 16 ? 1 : 2];
         if (e != hipSuccess || !F.wave_counts) return e;
         const int waves = F.num_tiles;  // one wave per tile, no splits

@@ -23,7 +23,7 @@ using rtt::Counts;
 namespace {
 
 // Waves per SIMD the register budget must allow: 6 (80 VGPRs, fewer spills in
-// the level loop) for up to 16 spp, 8 (64 VGPRs) above.  Measured (round 3,
+// the level loop) for up to 16 spp, 7 (72 VGPRs) above (8 until round 5).  Measured (round 3,
 // interleaved A/B): C4 (16 spp, depth 8) 6 waves -5 % single frame / -8 %
 // frames in flight against 7; C5 (64 spp, depth 16) 6 waves +2 %, 5 waves
 // +6 % against 7; 8 waves -1.1 % against 7 (r04l).
@@ -35,7 +35,7 @@ constexpr int kLvWavesLowSpp = 6;
 #ifdef RT_EXP_LVHIGH
 constexpr int kLvWavesHighSpp = RT_EXP_LVHIGH;  // measuring builds only
 #else
-constexpr int kLvWavesHighSpp = 8;
+constexpr int kLvWavesHighSpp = 7;  // r05k, with the fixed 64-spp shape: C5 -1.9 % against 8
 #endif
 
 // Level-synchronous all-packet megakernel (the default non-counting path on
