@@ -161,7 +161,8 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     frames only when no frame of another stream runs beside them (lpt_prepare
     overlapped_frame; `in_flight` False: frames one at a time) — Q4 for 2x2
     spp, W the waves per SIMD (5 for shards of <= 70,000 tiles and deep
-    frames, else 6).  The bench's timed frames are in flight (four streams):
+    frames, else 6), and a sixth argument `true` for the lone-shard instance
+    whose one-sample waves trace with the whole wave (csrc/coop.h).  The bench's timed frames are in flight (four streams):
     whole frames run the non-split instance."""
     if mode == "packet":
         return "render_packet_kernel<false, true>"
@@ -180,9 +181,11 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     tiles = -(-res_x // tw) * -(-local_rows // th)
     split = not deep and ((16 % spp == 0 and tiles <= 24000) or (4 % spp == 0 and (tiles <= 70000 or not in_flight)))
     waves = 5 if deep or (split and tiles <= 70000) else 6
+    # a lone shard of <= 40,000 tiles at 4 spp: one-sample waves, the SAMPLE instance
+    sample = split and not in_flight and spp == 4 and tiles <= 40000
     b = lambda v: "true" if v else "false"  # noqa: E731
     return (f"render_kernel<false, {b(split)}, {b(deep)}, {b(spp == 4 and tw == 4 and th == 4 and not deep)}, "
-            f"{waves}>")
+            f"{waves}{', true' if sample else ''}>")
 
 
 def host_facts():
@@ -587,12 +590,14 @@ def main():
     # end (rt_finish) — with frames in flight, the device time per launch of
     # the instance the timed frames run (the roofline's kernel time)
     kernel_ms = st.kernel_ms
+    timed_launch = ctx.last_launch()  # the instance and split shape the last timed frame ran (RT_DEBUG_LAST_LAUNCH)
     # a lone frame's kernel time (the same frames back to back on one stream,
     # no gather): such frames split their slowest tiles, so this is the split
     # instance — what one synchronous Update() frame costs
     for _ in range(args.steps):
         ctx.render_device(fr.camera, fr.plane, aparams, out.data_ptr(), nbytes)
     lone_kernel_ms = ctx.finish().kernel_ms
+    lone_launch = ctx.last_launch()
 
     # a moving camera (N = 1): every frame from another viewpoint, so the
     # longest-first order always comes from earlier, different frames
@@ -726,6 +731,8 @@ def main():
                 "shadow_rays_moot": moot // args.steps,
                 "mrays_per_s_traversed": (rays - moot) / elapsed / 1e6,
                 "frames_in_flight": nstreams,
+                "timed_launch": timed_launch,
+                "lone_launch": lone_launch,
                 "frames_per_gather": G if dist_on else None,
                 # device time per timed frame (HIP events over the timed frames)
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,

@@ -454,6 +454,12 @@ float rt_spec_threshold(void);
  * shape (tiles, split16 / split tiles, one-sample shift, rows, band), as
  * NUL-terminated text — which instance a frame took (tests, bench.py). */
 #define RT_DEBUG_LAST_LAUNCH 5
+/* Testing only: RT_DEBUG_SAMPLE_WAVE_STACK (value n >= 0; 0, the default:
+ * the whole area) limits the one-sample waves' whole-wave traversal to n
+ * stack entries for its 16-entries-a-step wide steps; above that it walks
+ * depth-first, one entry a step (csrc/coop.h) — a small n exercises that
+ * mode (same answers either way). */
+#define RT_DEBUG_SAMPLE_WAVE_STACK 6
 int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value);
 int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, int64_t *bytes_written);
 

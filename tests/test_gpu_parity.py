@@ -331,6 +331,36 @@ def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
             assert sr.shadow_rays_moot <= st.shadow_rays_moot <= st.shadow_rays, kw
 
 
+@pytest.mark.parametrize("name", ["C1", "C2", "C3", "C5"])
+@pytest.mark.parametrize("cap", [0, 40, 1])
+def test_one_sample_waves_trace_with_the_whole_wave(gpu_ctx, rt, name, cap):
+    """A lone shard's slowest pixels run as one-sample waves whose whole wave
+    traces the sample's ray chain (trace.hip render_sample_wave, coop.h: 16
+    stack entries tested per step, four lanes each): same bits and ray counts
+    as row-major frames, on the mesh / sphere / loose-triangle scenes (C5 at 4
+    spp, the megakernel's), with wide steps up to the whole stack area (cap
+    0), up to 40 entries (a mix of wide and depth-first steps) and never (1:
+    every step depth-first, one entry)."""
+    fr = rt.make(name)
+    if fr.spp != 4:
+        fr = fr.with_(spp=4)
+    fr = fr.with_resolution(480, 270)
+    gpu_ctx.set_scene(fr.scene)
+    lib = gpu_ctx.lib
+    assert lib.rt_debug_set(gpu_ctx.h, rt.abi.RT_DEBUG_SAMPLE_WAVE_STACK, cap) == 0
+    try:
+        for kw in ({}, dict(band_index=2, band_count=3, band_rows=8)):
+            row, sr = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
+            for _ in range(3):  # the first frame measures and sorts; later ones split
+                img, st = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr, **kw))
+                assert np.array_equal(img.view(np.uint32), row.view(np.uint32)), kw
+                assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == (sr.primary_rays, sr.shadow_rays,
+                                                                                 sr.reflection_rays), kw
+            assert "s16_shift=0" in gpu_ctx.last_launch(), gpu_ctx.last_launch()
+    finally:
+        assert lib.rt_debug_set(gpu_ctx.h, rt.abi.RT_DEBUG_SAMPLE_WAVE_STACK, 0) == 0
+
+
 def test_split_sixteenths_of_large_shards_is_invisible(gpu_ctx, rt):
     """Shards of 24,000-70,000 tiles (a 1/2 and a 1/4 shard of 1080p C3) run
     their slowest tiles finely split — synchronous (lone) frames their slowest

@@ -11,6 +11,7 @@
 #   pmc      counter passes of the C3 trace kernel (tools/pmc_round.sh)
 #   pmcall   counter passes C3 whole + 1/2, 1/4, 1/8 shares, C4, C5 (+ 1/8)
 #   sb       one rank's share at N = 2/4/8 (four streams and one)
+#   sbab     one rank's share, AB_VARIANTS alternated (SBAB_ROUNDS, SBAB_BANDS, SBAB_STREAMS, SBAB_STEPS)
 #   cfg      C4 / C5 bench lines (whole frame and 1/8 share)
 #   abx      interleaved A/B: AB_VARIANTS (default "base,default") on C3, C2, C4, C5 and C3 shares
 #   e2e      rt_render end to end (RGBA8 and float)
@@ -94,6 +95,27 @@ if has sb; then
       > $out/sb${n}s1_$tag.log 2>&1 || fail sb${n}s1 $out/sb${n}s1_$tag.log
   done
   echo sb-ok
+fi
+if has sbab; then
+  # one rank's share, library variants alternated (AB_VARIANTS; bench.py --lib)
+  for r in $(seq ${SBAB_ROUNDS:-2}); do
+    for v in ${AB_VARIANTS//,/ }; do
+      lib=""
+      [ "$v" != default ] && lib="--lib $v"
+      for n in ${SBAB_BANDS:-2 4 8}; do
+        for s in ${SBAB_STREAMS:-4 1}; do
+          f=$out/sbab_${tag}_${v}_${n}_${s}_$r.log
+          timeout -k 10 300 python bench.py --steps ${SBAB_STEPS:-200} --warmup 5 --no-cpu-baseline --sim-bands $n \
+            --streams $s $lib > $f 2>&1 || fail sbab-$v-$n-$s $f
+          grep '^{' $f | tail -1 | python3 -c "import sys, json; d = json.loads(sys.stdin.read()); \
+print(json.dumps({'variant': '$v', 'bands': $n, 'streams': $s, 'round': $r, 'ms_per_step': round(d['ms_per_step'], 5), \
+'kernel_ms': round(d['config']['kernel_ms_per_frame'], 5), 'launch': d['config'].get('timed_launch')}))" \
+            >> $out/sbab_$tag.jsonl
+        done
+      done
+    done
+  done
+  cat $out/sbab_$tag.jsonl
 fi
 if has cfg; then
   for c in C2 C4 C5; do

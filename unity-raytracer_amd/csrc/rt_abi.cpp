@@ -349,6 +349,11 @@ int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value) {
         for (int i = 0; i < nmembers(ctx); ++i) member(ctx, i)->debug_group_sample_waves = value != 0;
         return RT_OK;
     }
+    if (what == RT_DEBUG_SAMPLE_WAVE_STACK) {
+        if (value < 0) return fail(ctx, RT_E_INVALID, "RT_DEBUG_SAMPLE_WAVE_STACK: capacity >= 0");
+        for (int i = 0; i < nmembers(ctx); ++i) member(ctx, i)->debug_sample_wave_stack = value;
+        return RT_OK;
+    }
     if (what == RT_DEBUG_FAIL_SLAB) {
         ctx->debug_fail_slab = value;
         return RT_OK;

@@ -268,6 +268,11 @@ struct FrameDev {
     int s16_shift;
     float *split_samples;
     int *split_count;
+    // one-sample waves (trace.hip render_sample_wave): the stack depth up to
+    // which their traversal takes wide steps (coop.h), 0 = as deep as the
+    // wave's LDS stack area allows (testing knob: a small value makes every
+    // step depth-first, rt_debug_set)
+    int sample_wave_stack;
     // measuring builds only (RT_EXP_PERSIST): a whole frame's non-split launch
     // as persist_waves resident waves pulling longest-first tiles from eight
     // per-XCD tile counters (persist_ctr, 16 ints apart, zeroed per launch)

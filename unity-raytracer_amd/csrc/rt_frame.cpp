@@ -149,6 +149,7 @@ int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane
     F.tiles_x = (F.res_x + tw - 1) / tw;
     F.tiles_x_magic = F.tiles_x <= 1 ? 0xffffffffu : (unsigned)((1ull << 32) / (unsigned long long)F.tiles_x);
     F.s16_shift = 2;  // finely split tiles: a pixel per wave (lpt_prepare may choose a sample per wave)
+    F.sample_wave_stack = ctx->debug_sample_wave_stack;  // 0: the wave's whole LDS stack area
     const int tiles_y = (F.local_rows + th - 1) / th;
     F.num_tiles = F.res_x > 0 ? F.tiles_x * tiles_y : 0;
     const bool f8 = (prm->flags & RT_FLAG_OUT_RGBA8) != 0, f16 = (prm->flags & RT_FLAG_OUT_RGBA16F) != 0,

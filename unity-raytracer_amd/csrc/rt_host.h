@@ -365,6 +365,7 @@ struct rt_ctx {
     // rt_debug_set(RT_DEBUG_WAVE_CLOCKS), measuring builds: the last render_kernel launch's per-wave clocks
     bool debug_wave_clock = false;
     bool in_group_frame = false;  // rendering one band of a multi-device frame (rt_group.cpp group_frame)
+    int debug_sample_wave_stack = 0;  // rt_debug_set(RT_DEBUG_SAMPLE_WAVE_STACK, n): one-sample waves' wide-step limit (testing)
     bool debug_group_sample_waves = true;  // rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0): group bands without them
     std::atomic<bool> destroying{false};  // rt_destroy has begun (host_waits_report skips the context)
     std::string last_launch;  // the last render launch's kernel instance and split shape (RT_DEBUG_LAST_LAUNCH)

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include "coop.h"
 #include "kernels.h"
 #include "packet.h"
 #include "rt_device.h"
@@ -446,11 +447,141 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
 }
 
 
+// Shade (RayTracingSetup.cs:304-366) of one camera sample with every lane of
+// the wave on it: the same operations as shade_path / shade_levels (values
+// equal in all lanes), each closest-hit and shadow query a whole-wave
+// traversal.  The mirror fold (c + km*(...), back to front) sits in the
+// wave's LDS: `fold` holds 6 floats per level (kMaxBounces levels).  Tallies
+// are wave-uniform.
+__device__ __forceinline__ f3 shade_wave(const SceneDev &S, const FrameDev &F, f3 o, f3 d, int2 *stk, int wide,
+                                         float *fold, unsigned &n_sh, unsigned &n_rf, unsigned &n_mo) {
+    int depth = 0;
+    f3 term;
+    while (true) {
+        rtt::RayCtx r;
+        rtt::setup_ray(r, o, d);
+        float bt;
+        int br;
+        if (!rtc::traverse_wave<false>(S, r, 0.0f, 0.0f, bt, br, stk, wide)) {  // :310-311
+            term = rtt::ld3(F.bg255);
+            break;
+        }
+        const rts::Surface sf = rts::surface(S, o, d, bt, br);
+        f3 col = rts::ambient(S, S.mats[sf.mat]);
+        for (int l = 0; l < S.num_lights; ++l) {  // :327-356
+            const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
+            ++n_sh;
+            // a moot shadow ray (shade.h same_bits) is not traced
+            const f3 lit = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
+            if (rts::same_bits(lit, col)) {
+                ++n_mo;
+                continue;
+            }
+            rtt::RayCtx rs;
+            rtt::setup_ray(rs, sr.o, sr.dir);
+            float dt;
+            int dr;
+            if (!rtc::traverse_wave<true>(S, rs, sqrtf(sr.d2) * 1.001f, sr.d2, dt, dr, stk, wide)) col = lit;
+        }
+        const DevMaterial m = S.mats[sf.mat];
+        if (m.ka_mirror.w != 0.0f && depth < F.max_bounces) {  // :358-363
+            float *q = fold + depth * 6;  // every lane stores the same values
+            q[0] = col.x;
+            q[1] = col.y;
+            q[2] = col.z;
+            q[3] = m.km.x;
+            q[4] = m.km.y;
+            q[5] = m.km.z;
+            rts::reflect(sf, o, d);
+            ++depth;
+            ++n_rf;
+            continue;
+        }
+        term = col;
+        break;
+    }
+    for (int k = depth - 1; k >= 0; --k) {
+        const float *q = fold + k * 6;
+        term = mk(q[0], q[1], q[2]) + mk(q[3], q[4], q[5]) * term;
+    }
+    return term;
+}
+
+// A one-sample wave (a lone shard's finely split tile, F.s16_shift 0): the
+// sample render_tile's lane `part` would trace, traced by the whole wave
+// (shade_wave), then the same write-through hand-off to the pixel's other
+// three samples.  Returns true when the sample was answered by the sky test.
+template <bool Q4>
+__device__ __forceinline__ bool render_sample_wave(const SceneDev &S, const FrameDev &F, const rtt::Stack &st,
+                                                   int *fold_lds, int tile, int part, int sidx, Counts &cnt) {
+    constexpr int FX = Q4 ? 2 : 0;
+    int px, ly, gy, s;
+    const bool active = rts::slot_pixel<FX>(F, tile, part, px, ly, gy, s);
+    // render_tile's sky test of its one active lane
+    const bool sky = !(active && (!F.sky_test || rts::sky_maybe<FX>(F, px, gy, s)));
+    if (!active) return sky;
+    unsigned n_sh = 0, n_rf = 0, n_mo = 0;
+    f3 color;
+    if (sky) {
+        color = rtt::ld3(F.bg255);  // :310-311
+    } else {
+        f3 o, d;
+        rts::primary_ray<FX>(F, px, gy, s, o, d);
+        // the wave's per-lane LDS stack area, free in a one-sample wave, holds the wave's stack
+        int2 *stk = reinterpret_cast<int2 *>(st.lds);
+        const int full = st.n * kWaveSize / 2 - rtc::kStackReserve;
+        const int knob = __builtin_amdgcn_readfirstlane(F.sample_wave_stack);
+        color = shade_wave(S, F, o, d, stk, knob > 0 && knob < full ? knob : full, reinterpret_cast<float *>(fold_lds), n_sh,
+                           n_rf, n_mo);
+    }
+    if (rtt::lane_id() == 0) {
+        cnt.shadow += n_sh;
+        cnt.reflection += n_rf;
+        cnt.moot += n_mo;
+        // render_tile's hand-off, for the sample of lane `part`
+        typedef __attribute__((address_space(1))) unsigned gu32;
+        typedef __attribute__((address_space(1))) int gi32;
+        float *sp = F.split_samples + ((size_t)sidx * kWaveSize + part) * 4;
+        __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int *cp = F.split_count + sidx * (kWaveSize / 4) + (part >> 2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
+        if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
+            const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (part & ~3)) * 4;
+            auto ld = [](const float *q) {
+                return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            };
+            f3 v = mk(ld(b), ld(b + 1), ld(b + 2));
+            for (int k = 1; k < 4; ++k) v = v + mk(ld(b + 4 * k), ld(b + 4 * k + 1), ld(b + 4 * k + 2));
+            v = v * 0.25f;
+            rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+            __hip_atomic_store((gi32 *)cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
+        }
+    }
+    return sky;
+}
+
+// One-sample waves traced by the whole wave (render_sample_wave, the SAMPLE
+// instances); measuring builds may switch it off (-DRT_EXP_NOCOOP: the
+// sample's lane alone, render_tile).
+#ifdef RT_EXP_NOCOOP
+constexpr bool kCoopSampleWaves = false;
+#else
+constexpr bool kCoopSampleWaves = true;
+#endif
+
 // SPLIT: the variant launched when a frame splits tiles (a separate instance, so
 // the common kernel's code and register allocation stay as they are); DEEP:
 // the one for MaxReflectionBounces > kMaxBounces (deep_chain); Q4: frames of
-// 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel).
-template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false, int W = kMkMinWaves>
+// 2x2 spp in 4x4-pixel tiles (shade.h primary_ray / slot_pixel); SAMPLE:
+// the lone-shard frames whose finely split tiles run as one-sample waves
+// (F.s16_shift 0), each traced by its whole wave (render_sample_wave) — its
+// own instance, so the shard instance that frames in flight run keeps its
+// register allocation (the whole-wave path beside it: +11 VGPR and +65 SGPR
+// spill slots, in-flight 1/2 and 1/4 shares 9-14 % slower, r05n).
+template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false, int W = kMkMinWaves,
+          bool SAMPLE = false>
 __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, FrameDev F) {
     // the per-lane LDS stack: kStackSize entries where six waves per SIMD must
     // fit the CU's LDS, kStackShard at five (fewer overflows to scratch)
@@ -541,8 +672,14 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     // the shadow occluder hints (packet.h HINT) pay off in small frames only:
     // the 5-wave split instance (row shards), not the whole-frame one
     constexpr bool HINT = SPLIT && W < 6;
-    const bool sky =
-        render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, idx);
+    bool sky;
+    // a one-sample wave (pshift 0: render_tile's hand-off case) with its whole
+    // wave on the sample's ray chain (wave-uniform test)
+    if (SAMPLE && kCoopSampleWaves && HINT && !COUNT && !DEEP && pshift == 0 && (Q4 || F.spp == 4) && S.bvh4 &&
+        F.max_bounces <= kMaxBounces)
+        sky = render_sample_wave<Q4>(S, F, st, wstack, tile, part, idx, cnt);
+    else
+        sky = render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, idx);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
@@ -943,10 +1080,15 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
             RT_LAUNCH((render_kernel<false, false, true, false, W5>), "render_kernel<false, false, true, false, 5>");
     } else if (count_tests)
         RT_LAUNCH((render_kernel<true, false, false, false, W5>), "render_kernel<true, false, false, false, 5>");
+    else if (split && q4 && shard && F.s16_shift == 0)
+        RT_LAUNCH((render_kernel<false, true, false, true, W5, true>), "render_kernel<false, true, false, true, 5, true>");
     else if (split && q4 && shard)
         RT_LAUNCH((render_kernel<false, true, false, true, W5>), "render_kernel<false, true, false, true, 5>");
     else if (split && q4)
         RT_LAUNCH((render_kernel<false, true, false, true>), "render_kernel<false, true, false, true, 6>");
+    else if (split && shard && F.s16_shift == 0)
+        RT_LAUNCH((render_kernel<false, true, false, false, W5, true>),
+                  "render_kernel<false, true, false, false, 5, true>");
     else if (split && shard)
         RT_LAUNCH((render_kernel<false, true, false, false, W5>), "render_kernel<false, true, false, false, 5>");
     else if (split)
