@@ -231,6 +231,16 @@ constexpr int kSplit16Div = RT_EXP_SPLIT16DIV;  // measuring builds only
 constexpr int kSplit16Div = 2048;  // of those, 1/kSplit16Div of the tiles as sixteenth-waves; 0: off
 #endif
 constexpr int kSplitDiv = 256;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
+// A lone shard's finely split tiles run as one-sample waves traced by the
+// whole wave (trace.hip render_sample_wave, csrc/coop.h): cheap enough to
+// split its slowest 1/256 so (1/1024 before the whole-wave traversal: the
+// rest of a 1/8 C3 share's slowest waves were whole tiles of ~105 us):
+// single frame -13 % on two 1/8 shares against 1/1024 (r05q).
+#ifdef RT_EXP_SPLIT16SAMPLE
+constexpr int kSplit16DivSample = RT_EXP_SPLIT16SAMPLE;  // measuring builds only
+#else
+constexpr int kSplit16DivSample = 256;
+#endif
 // Larger shards (up to 70,000 tiles: a 1/2 or 1/4 shard of 1080p) split only
 // their slowest 1/4096 into sixteenth-waves: single frame -15..-30 %,
 // throughput with frames in flight +2..4 % on a 1/4 shard; a whole frame
@@ -264,10 +274,16 @@ constexpr int kSample16LoneTiles = 40000;  // lone shards up to this many tiles:
 // overlapped_frame: a synchronous Update() frame of one rank) its slowest
 // 1/1024: a 1/2 C3 shard's single frame -10.6 %, frames in flight +-0 (r04n;
 // its slowest waves were whole tiles of ~190 us against a 148-us dispatch).
+// One whose split tiles run as one-sample waves (<= kSample16LoneTiles: a 1/4
+// shard) 1/512 since those trace with the whole wave (its slowest waves were
+// then whole tiles of 120-130 us, wclk_r05p): -12.5 % and +1.4 % on two 1/4
+// shares (r05q).
 #ifdef RT_EXP_SPLIT16LONE
 constexpr int kSplit16DivLone = RT_EXP_SPLIT16LONE;  // measuring builds only
+constexpr int kSplit16DivLoneSample = RT_EXP_SPLIT16LONE;
 #else
 constexpr int kSplit16DivLone = 1024;
+constexpr int kSplit16DivLoneSample = 512;
 #endif
 #ifdef RT_EXP_NOSYNCSPLIT
 constexpr bool kSplitSync = false;  // measuring builds only
@@ -456,17 +472,20 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         F.split_tiles = std::max(1, F.num_tiles / kSplitDiv);
         // sixteenth-waves (4 lanes) must hold whole pixels too
         if (kSplit16Div > 0 && 4 % F.spp == 0) {
-            // a lone shard's (one-sample waves, below) twice as many: a 1/8
-            // C3 share's single frame -11.9 %; in flight +2.6 % (r04av)
+            // a lone shard's (one-sample waves, below) more (kSplit16DivSample)
             const bool sample_waves = F.spp == 4 && !overlapped_frame(ctx, prm) && group_sample_waves(ctx);
-            const int div = sample_waves ? kSplit16Div / 2 : kSplit16Div;
+            const int div = sample_waves ? kSplit16DivSample : kSplit16Div;
             F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / div));
             F.split_tiles -= F.split16_tiles;
         }
     } else if (F.tile_order && !count && !levels && kSplit16DivLarge > 0 && 4 % F.spp == 0 &&
                (F.num_tiles <= kSplit16MaxTiles || (kSplitSync && !overlapped_frame(ctx, prm)))) {
         const bool lone_shard = F.num_tiles <= kSplit16MaxTiles && !overlapped_frame(ctx, prm);
-        const int div = lone_shard ? kSplit16DivLone : F.num_tiles > kSplit16MaxTiles ? kSplit16DivWhole : kSplit16DivLarge;
+        // (one-sample waves below: kSplit16DivLoneSample)
+        const bool sample_waves = lone_shard && F.spp == 4 && F.num_tiles <= kSample16LoneTiles && group_sample_waves(ctx);
+        const int div = sample_waves ? kSplit16DivLoneSample
+                        : lone_shard ? kSplit16DivLone
+                        : F.num_tiles > kSplit16MaxTiles ? kSplit16DivWhole : kSplit16DivLarge;
         F.split16_tiles = std::max(1, F.num_tiles / div);
     }
     // the split-tile instance's shadow occluder hints (packet.h packet_trace
