@@ -591,6 +591,7 @@ def main():
     # the instance the timed frames run (the roofline's kernel time)
     kernel_ms = st.kernel_ms
     timed_launch = ctx.last_launch()  # the instance and split shape the last timed frame ran (RT_DEBUG_LAST_LAUNCH)
+    sky_tiles = int(timed_launch.split("sky=")[1].split()[0]) if "sky=" in timed_launch else 0
     # a lone frame's kernel time (the same frames back to back on one stream,
     # no gather): such frames split their slowest tiles, so this is the split
     # instance — what one synchronous Update() frame costs
@@ -748,7 +749,11 @@ def main():
                 # rank 0's host time per enqueued frame: near ms_per_step means host-bound
                 "host_enqueue_ms_per_frame": host_s / args.steps * 1e3,
             },
-            "roofline": {**roofline(pmc, pmc_state, kname, avg_kernel_s, logical), "canonical_counts": canonical},
+            "roofline": {**roofline(pmc, pmc_state, kname, avg_kernel_s, logical), "canonical_counts": canonical,
+                         # whole frames in flight: the order's sky tail in a second launch per frame
+                         # (trace.hip sky_batch_kernel); avg_kernel_ms and the counters cover both
+                         **({"with": f"sky_batch_kernel<{'true' if fr.spp == 4 else 'false'}>",
+                             "with_tiles": sky_tiles} if sky_tiles else {})},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(rt, fr, args.cpu_seconds, ctx)

@@ -331,6 +331,59 @@ def test_split_slowest_tiles_is_invisible(gpu_ctx, rt):
             assert sr.shadow_rays_moot <= st.shadow_rays_moot <= st.shadow_rays, kw
 
 
+@pytest.mark.parametrize("res", [(480, 270), (1920, 1080)])
+def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res):
+    """Frames in flight (another stream's frame beside them) take the last
+    measured order's sky tail kSkyBatch tiles a wave (trace.hip
+    sky_batch_kernel, RT_DEBUG_LAST_LAUNCH "sky=N"; lone frames do not).  After
+    the camera moves the order is stale until the next re-sort: tiles of that
+    tail now show the knot and are rendered in full.  Frames equal row-major
+    frames bit for bit, with the same ray counts, before and after the move."""
+    import torch
+    fr = rt.make("C3").with_resolution(*res)
+    ctx = gpu_ctx
+    ctx.set_scene(fr.scene)
+    c = fr.camera
+    moved = rt.CameraData(tuple(float(a + 1.5 * b) for a, b in zip(c.Position, c.Right)), c.Forward, c.Right, c.Up)
+    prow = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER)
+    row, sr = ctx.render(c, fr.plane, prow)
+    row2, sr2 = ctx.render(moved, fr.plane, prow)
+    assert not np.array_equal(row2.view(np.uint32), row.view(np.uint32))
+    H, W = fr.plane.ResolutionY, fr.plane.ResolutionX
+    outs = [torch.empty((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    pa = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC)
+    rays = lambda s: (s.primary_rays, s.shadow_rays, s.reflection_rays)  # noqa: E731
+
+    def pair(cam0):  # a static-camera frame on stream 1, then the frame under test on stream 0 beside it
+        for k, cam in ((1, c), (0, cam0)):
+            ctx.set_stream(streams[k].cuda_stream)
+            ctx.render_device(cam, fr.plane, pa, outs[k].data_ptr(), outs[k].numel() * 4)
+        launch = ctx.last_launch()
+        st = ctx.finish()
+        torch.cuda.synchronize()
+        return launch, st, [o.cpu().numpy() for o in outs]
+
+    try:
+        for k in range(3):  # frame 0 of each stream measures and sorts; later frames take batches
+            launch, st, img = pair(c)
+            for i in range(2):
+                assert np.array_equal(img[i].view(np.uint32), row.view(np.uint32)), (k, i)
+            assert rays(st) == tuple(2 * v for v in rays(sr)), k
+        assert int(launch.split("sky=")[1].split()[0]) > 0, launch
+        launch, st, img = pair(moved)  # the same (now stale) order, each stream's frame 3 of 16
+        assert int(launch.split("sky=")[1].split()[0]) > 0, launch
+        assert np.array_equal(img[1].view(np.uint32), row.view(np.uint32))
+        assert np.array_equal(img[0].view(np.uint32), row2.view(np.uint32))
+        assert rays(st) == tuple(a + b for a, b in zip(rays(sr), rays(sr2)))
+        # a lone frame takes no batches
+        ctx.set_stream(None)
+        ctx.render(c, fr.plane, rt.frame_params(fr))
+        assert "sky=0" in ctx.last_launch(), ctx.last_launch()
+    finally:
+        ctx.set_stream(None)
+
+
 @pytest.mark.parametrize("name", ["C1", "C2", "C3", "C5"])
 @pytest.mark.parametrize("cap", [0, 40, 1])
 def test_one_sample_waves_trace_with_the_whole_wave(gpu_ctx, rt, name, cap):

@@ -66,7 +66,8 @@ fi
 if has kt; then
   cd /tmp
   # the bench's timed frames (no moving camera: the in-flight instance's last 50 launches are the timed
-  # frames; tools/kt_span.py --last 50 gives their device time per launch, bench.py's roofline.avg_kernel_ms)
+  # frames; tools/kt_span.py --last 50 --with sky_batch_kernel gives their device time per frame, bench.py's
+  # roofline.avg_kernel_ms)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/kt_$tag -o run --output-format csv -- \
     python3 $R/bench.py --steps 50 --warmup 5 --no-cpu-baseline --moving-frames 0 > $R/$out/kt_$tag.log 2>&1 \
     || fail kt $R/$out/kt_$tag.log

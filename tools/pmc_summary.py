@@ -22,8 +22,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def load(dirs):
     """kernel -> counter -> [per-dispatch values], over the dispatches of the
-    kernel's largest grid only: the workload's launches, not the tiny warm-up
-    frames a context renders at its first rt_set_scene (same kernel names)."""
+    kernel's most frequent grid only: the workload's launches, not the tiny
+    warm-up frames a context renders at its first rt_set_scene (same kernel
+    names), nor a stream's first frame before its longest-first order exists
+    (whose whole-frame launch has no sky tail: a larger grid)."""
     vals = defaultdict(lambda: defaultdict(list))
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -34,11 +36,12 @@ def load(dirs):
                 names[did] = row["Kernel_Name"]
                 grids[did] = int(float(row.get("Grid_Size") or 0))
                 per[did][row["Counter_Name"]] += float(row["Counter_Value"])
-            biggest = defaultdict(int)
+            freq = defaultdict(lambda: defaultdict(int))
             for did, g in grids.items():
-                biggest[names[did]] = max(biggest[names[did]], g)
+                freq[names[did]][g] += 1
+            mode = {k: max(v.items(), key=lambda gv: (gv[1], gv[0]))[0] for k, v in freq.items()}
             for did, cs in per.items():
-                if grids[did] != biggest[names[did]]:
+                if grids[did] != mode[names[did]]:
                     continue
                 for c, v in cs.items():
                     vals[names[did]][c].append(v)
@@ -49,6 +52,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--kernel", default="render_kernel<false>")
+    ap.add_argument("--with", dest="with_", default="",
+                    help="a kernel launched once per frame beside --kernel (sky_batch_kernel): its per-dispatch "
+                         "counters are added, the per-frame figures cover both")
     ap.add_argument("--out", default="")
     ap.add_argument("--config", default="", help="recorded: the config the counters were taken on")
     ap.add_argument("--bands", type=int, default=1, help="recorded: row band 0 of N (one rank's share)")
@@ -64,6 +70,11 @@ def main():
     res = {"kernels": summary, "config": a.config or None, "bands": a.bands}
     if pick:
         name, c = max(pick.items(), key=lambda kv: len(kv[1]))
+        comp = {k: v for k, v in summary.items() if a.with_ and a.with_ in k}
+        if comp:
+            wname, wc = max(comp.items(), key=lambda kv: len(kv[1]))
+            c = {k: c.get(k, 0.0) + wc.get(k, 0.0) for k in set(c) | set(wc)}
+            res["with"] = wname
         rd = None
         if "TCC_EA0_RDREQ_32B" in c and "TCC_EA0_RDREQ_64B" in c and "TCC_EA0_RDREQ_128B" in c:
             rd = 32 * c["TCC_EA0_RDREQ_32B"] + 64 * c["TCC_EA0_RDREQ_64B"] + 128 * c["TCC_EA0_RDREQ_128B"]

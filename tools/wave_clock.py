@@ -53,6 +53,12 @@ def analyse(rec):
         "split_waves": int(np.sum(part >= 0)),
         "top_waves_us": [round(int(x) * TICK_US, 1) for x in np.sort(dur)[::-1][:16]],
         "top_waves_split": [int(part[i]) for i in np.argsort(dur)[::-1][:16]],
+        # waves by duration (us bins): count and summed wave time — what the
+        # short (sky) waves cost the launch against the long ones
+        "dur_bins_us": [0, 2, 4, 8, 16, 32, 64, 128, 1e9],
+        "dur_bin_waves": np.histogram(dur * TICK_US, [0, 2, 4, 8, 16, 32, 64, 128, 1e9])[0].tolist(),
+        "dur_bin_busy_us": [round(float(dur[(dur * TICK_US >= lo) & (dur * TICK_US < hi)].sum()) * TICK_US, 1)
+                            for lo, hi in zip([0, 2, 4, 8, 16, 32, 64, 128], [2, 4, 8, 16, 32, 64, 128, 1e9])],
     }
 
 

@@ -17,6 +17,21 @@ constexpr bool kWaveClockBuild = true;
 constexpr bool kWaveClockBuild = false;
 #endif
 
+// Sky tiles per wave at the end of a longest-first order (FrameDev
+// sky_batch_tiles): a tile whose every sample surely misses the scene box is
+// a background store, too little work for a wave of its own (60 % of a C3
+// frame's waves, 12 % of its wave time: wclk_r05s).
+#ifdef RT_EXP_SKYBATCH
+constexpr int kSkyBatch = RT_EXP_SKYBATCH;  // measuring builds only (1: off)
+#else
+constexpr int kSkyBatch = 16;
+#endif
+// Count of the tiles before the sorted order's sky tail (cost key 0) into
+// host-mapped memory, one 64-bit store tagged with the sort's sequence number:
+// (seq << 32) | count.
+hipError_t launch_sky_count(const unsigned *cost_sorted, int n, unsigned seq, unsigned long long *out,
+                            hipStream_t stream);
+
 // Frames (row shards) of at most this many tiles launch render_kernel's
 // 5-wave instances (trace.hip), the only ones with the one-sample split path.
 constexpr int kShardTilesMax = 70000;

@@ -235,6 +235,7 @@ struct FrameDev {
     int out_format;          // kOutFloat4 / kOutRGBA8 / kOutRGBA16F / kOutRGB32F
     int split16_tiles;       // render_kernel: the first split16_tiles of tile_order run as 16 sixteenth-waves each,
     int split_tiles;         // ... the next split_tiles as 4 quarter-waves each
+    int sky_batch_tiles;     // ... and the last sky_batch_tiles (the last measurement's sky tiles) rtk::kSkyBatch a wave
     unsigned long long *counters;  // kCounterSlots x kCounterWords u64, rt_stats order
     // Conservative sky test (render_kernel, non-counting instances): a wave
     // whose every sample ray, approximated (relative error ~1e-6), misses the

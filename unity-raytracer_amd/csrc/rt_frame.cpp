@@ -422,10 +422,13 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
                 LptSlot *&ls, bool &lpt_sort) {
     ls = nullptr;
     lpt_sort = false;
+    ctx->last_lpt.clear();
     F.tile_order = nullptr;
     F.tile_cost = nullptr;
     F.wave_counts = nullptr;
-    if (!mega || (prm->flags & RT_FLAG_ROW_ORDER) != 0 || F.num_tiles <= 0) return RT_OK;
+    // (a counting launch measures tests, not costs: its per-lane walk is not the
+    // frame a longest-first order is for, and it never answers a tile as sky)
+    if (!mega || count || (prm->flags & RT_FLAG_ROW_ORDER) != 0 || F.num_tiles <= 0) return RT_OK;
     for (LptSlot &l : ctx->lpt)
         if (l.used && l.stream == ctx->stream && l.slab == slab) ls = &l;
     if (!ls)
@@ -449,6 +452,17 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         HIP_OR_FAIL(ctx, rtk::launch_iota((int *)ls->iota.p, F.num_tiles, ctx->stream));
         ls->key = key;
         ls->valid = false;
+        ls->sky_tail = 0;
+        ls->sky_pending = ls->sky_known = false;  // (a count still in flight is for the old layout)
+    }
+    // the sky tail of the last sort, once its count has reached the host (a
+    // plain read of host memory: the count arrives tagged with its sort)
+    if (ls->sky_pending) {
+        const unsigned long long v = *(volatile unsigned long long *)ls->sky_host;
+        if ((unsigned)(v >> 32) == ls->sky_seq) {
+            ls->sky_tail = std::max(0, std::min(F.num_tiles, F.num_tiles - (int)(unsigned)v));
+            ls->sky_pending = false;
+        }
     }
     if (ls->scene != ctx->scene_version) {
         // a new or updated scene (rt_update_mesh_transforms every Update): the
@@ -526,6 +540,22 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         F.split_samples = (float *)ls->split_samples.p;
         F.split_count = (int *)ls->split_count.p;
     }
+    // The sorted order ends with the tiles the last measurement found to be
+    // sky (cost key 0, row order): with other frames in flight beside this
+    // one, sky_batch_kernel takes them rtk::kSkyBatch a wave after
+    // render_kernel (C3 frames in flight -2.5 %, C2 -4.6 %; a lone frame, whose
+    // critical path the second launch lengthens, +0.5 % C3, +5 % a 1/8 shard:
+    // abx_r05t).  Only the grids depend on this count (a stale one costs time,
+    // not pixels: a batch renders any tile that is not sky in full).
+    if (F.tile_order && !count && !levels && rtk::kSkyBatch > 1 && F.num_tiles > rtk::kShardTilesMax &&
+        overlapped_frame(ctx, prm))
+        F.sky_batch_tiles = std::min(ls->sky_tail, F.num_tiles - F.split_tiles - F.split16_tiles);
+    {
+        char b[128];
+        snprintf(b, sizeof b, " lpt: frame=%lld sky_tail=%d known=%d pending=%d overlapped=%d", ls->frames,
+                 ls->sky_tail, (int)ls->sky_known, (int)ls->sky_pending, (int)overlapped_frame(ctx, prm));
+        ctx->last_lpt = b;
+    }
     if (levels && !(F.max_bounces > rtd::kMaxBounces)) {
         // the levels kernel dispatches XCD-aware stripes in row order
         // (trace_levels.hip): no longest-first order, no cost measurement
@@ -573,6 +603,29 @@ int lpt_sort_now(rt_ctx *ctx, const rtd::FrameDev &F, LptSlot *ls) {
                                              (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
                                              ls->scratch.p, ls->scratch.cap, ctx->stream));
     ls->valid = true;
+    if (rtk::kSkyBatch > 1) {
+        if (!ls->sky_host)
+            HIP_OR_FAIL(ctx, hipHostMalloc((void **)&ls->sky_host, sizeof(unsigned long long), hipHostMallocDefault));
+        unsigned long long *dev = nullptr;
+        HIP_OR_FAIL(ctx, hipHostGetDevicePointer((void **)&dev, ls->sky_host, 0));
+        HIP_OR_FAIL(ctx, rtk::launch_sky_count((const unsigned *)ls->cost_sorted.p, F.num_tiles, ++ls->sky_seq, dev,
+                                               ctx->stream));
+        ls->sky_pending = true;
+        if (!ls->sky_known) {
+            // the slot's first order: wait for its count once (frames in
+            // flight run far ahead of the device, so a lagged count of the
+            // first sort would arrive only after the frames that need it)
+            if (!ls->sky_ev) HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&ls->sky_ev, hipEventDisableTiming));
+            HIP_OR_FAIL(ctx, hipEventRecord(ls->sky_ev, ctx->stream));
+            HIP_WAIT(ctx, hipEventSynchronize(ls->sky_ev));
+            const unsigned long long v = *(volatile unsigned long long *)ls->sky_host;
+            if ((unsigned)(v >> 32) == ls->sky_seq) {
+                ls->sky_tail = std::max(0, std::min(F.num_tiles, F.num_tiles - (int)(unsigned)v));
+                ls->sky_pending = false;
+            }
+            ls->sky_known = true;
+        }
+    }
     return RT_OK;
 }
 
@@ -602,10 +655,11 @@ int launch_frame(rt_ctx *ctx, rtd::FrameDev &F, const Path &P, const rtw::Args &
         HIP_OR_FAIL(ctx, rtk::launch_render_mega(ctx->S, F, P.count, ctx->stream, &inst));
         if (inst) {  // rt_debug_read RT_DEBUG_LAST_LAUNCH
             char b[256];
-            snprintf(b, sizeof b, "%s tiles=%d split16=%d split=%d s16_shift=%d rows=%d band=%d/%d", inst,
+            snprintf(b, sizeof b, "%s tiles=%d split16=%d split=%d s16_shift=%d rows=%d band=%d/%d sky=%d", inst,
                      F.num_tiles, F.split16_tiles, F.split_tiles, F.s16_shift, F.local_rows, F.band_index,
-                     F.band_count);
+                     F.band_count, F.sky_batch_tiles);
             ctx->last_launch = b;
+            ctx->last_launch += ctx->last_lpt;
         }
     }
     else if (P.wavefront && F.num_tiles > 0)

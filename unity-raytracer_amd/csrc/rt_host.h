@@ -80,6 +80,14 @@ struct LptSlot {
     GrowBuf hints;        // render_kernel's shadow-packet occluder hints (rtd::FrameDev::shadow_hint)
     GrowBuf split_samples, split_count;  // one-sample split waves' hand-off (rtd::FrameDev::split_*)
     GrowBuf persist_ctr;                 // measuring builds (RT_EXP_PERSIST): per-XCD tile counters
+    // the sorted order's sky tail (render_kernel sky batches): counted on the
+    // device after each sort into host-mapped memory — awaited after the
+    // slot's first sort, later ones taken once their event has fired
+    unsigned long long *sky_host = nullptr;  // (sort sequence << 32) | tiles before the sky tail
+    hipEvent_t sky_ev = nullptr;
+    unsigned sky_seq = 0;
+    bool sky_pending = false, sky_known = false;
+    int sky_tail = 0;
     unsigned long long hints_scene = ~0ull;  // the scene version and layout the hints were recorded for
     long long hints_key = -1;
     long long key = -1;
@@ -93,6 +101,12 @@ struct LptSlot {
             b->p = nullptr;
             b->cap = 0;
         }
+        if (sky_ev) (void)hipEventDestroy(sky_ev);
+        if (sky_host) (void)hipHostFree(sky_host);
+        sky_ev = nullptr;
+        sky_host = nullptr;
+        sky_pending = sky_known = false;
+        sky_tail = 0;
     }
 };
 constexpr int kLptSlots = 16;  // streams x row slabs
@@ -368,7 +382,8 @@ struct rt_ctx {
     int debug_sample_wave_stack = 0;  // rt_debug_set(RT_DEBUG_SAMPLE_WAVE_STACK, n): one-sample waves' wide-step limit (testing)
     bool debug_group_sample_waves = true;  // rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0): group bands without them
     std::atomic<bool> destroying{false};  // rt_destroy has begun (host_waits_report skips the context)
-    std::string last_launch;  // the last render launch's kernel instance and split shape (RT_DEBUG_LAST_LAUNCH)
+    std::string last_launch;
+    std::string last_lpt;  // the longest-first slot's state of the last launch (RT_DEBUG_LAST_LAUNCH)  // the last render launch's kernel instance and split shape (RT_DEBUG_LAST_LAUNCH)
     rti::GrowBuf wave_clock;
     int64_t wave_clock_bytes = 0;
 };

@@ -562,6 +562,31 @@ __device__ __forceinline__ bool render_sample_wave(const SceneDev &S, const Fram
     return sky;
 }
 
+// A tile of a sky batch (render_kernel, the last F.sky_batch_tiles of the
+// order): render_tile's sky test — false when any sample may meet the scene
+// (the caller renders the tile in full) — and otherwise its background
+// pixels: the same samples (Shade's background, RayTracingSetup.cs:310-311),
+// the same in-order sum and mean as render_tile's sky tiles.
+template <bool Q4>
+__device__ __forceinline__ bool sky_tile(const FrameDev &F, int tile) {
+    constexpr int FX = Q4 ? 2 : 0;
+    int px, ly, gy, s;
+    const bool active = rts::slot_pixel<FX>(F, tile, rtt::lane_id(), px, ly, gy, s);
+    if (__ballot(active && (!F.sky_test || rts::sky_maybe<FX>(F, px, gy, s))) != 0) return false;
+    if (active && s == 0) {
+        const f3 bg = rtt::ld3(F.bg255);
+        const int spp = Q4 ? 4 : F.spp;
+        f3 v = bg;
+        for (int k = 1; k < spp; ++k) v = v + bg;  // rts::sample_sum's order
+        if (Q4)
+            v = v * 0.25f;
+        else if (F.spp > 1)
+            v = (F.spp & (F.spp - 1)) == 0 ? v * F.inv_spp : v / (float)F.spp;
+        rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+    }
+    return true;
+}
+
 // One-sample waves traced by the whole wave (render_sample_wave, the SAMPLE
 // instances); measuring builds may switch it off (-DRT_EXP_NOCOOP: the
 // sample's lane alone, render_tile).
@@ -637,7 +662,9 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     const int split16 = SPLIT ? F.split16_tiles : 0;
     const int split = SPLIT ? F.split_tiles : 0;
     const int s16sh = SPLIT ? s16_shift(F) : 2;  // one finely split tile: 64 >> s16sh waves
-    if (wid >= F.num_tiles + ((64 >> s16sh) - 1) * split16 + 3 * split) return;  // wave-uniform
+    // (the order's last F.sky_batch_tiles positions: sky_batch_kernel's)
+    if (wid >= F.num_tiles - (COUNT ? 0 : F.sky_batch_tiles) + ((64 >> s16sh) - 1) * split16 + 3 * split)
+        return;  // wave-uniform
 #ifdef RT_WAVE_CLOCK
     const unsigned long long rc0 = __builtin_amdgcn_s_memrealtime();  // constant 100 MHz clock
 #endif
@@ -730,6 +757,39 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
         rtt::flush_counts<COUNT>(cnt, F.counters);
     }
 #endif
+}
+
+// The sky tail of a longest-first order (the last F.sky_batch_tiles
+// positions: the tiles the last measurement found to be sky), rtk::kSkyBatch
+// tiles a wave, launched after render_kernel on its stream.  A sky tile is a
+// background store (sky_tile), too little work for a wave of its own: 60 % of
+// a whole C3 frame's waves and 12 % of its wave time were such tiles
+// (wclk_r05s).  A tile that is not sky this frame (the order predates a
+// camera or scene change) is rendered in full, as render_kernel's whole-frame
+// instance would; its tallies go to the counters directly.
+template <bool Q4>
+__global__ __launch_bounds__(kMkThreads, kMkMinWaves) void sky_batch_kernel(SceneDev S, FrameDev F) {
+    __shared__ int stack_mem[kStackSize * kWaveSize];
+    __shared__ int wstack_mem[rtp::kWaveStack];
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem, ovf, kStackSize};
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    const int p0 = F.num_tiles - F.sky_batch_tiles + (int)blockIdx.x * rtk::kSkyBatch;
+    const int n = min(rtk::kSkyBatch, F.num_tiles - p0);  // wave-uniform
+    for (int j = 0; j < n; ++j) {
+        const int tile = __builtin_amdgcn_readfirstlane(rtt::cload(F.tile_order + p0 + j));
+        if (sky_tile<Q4>(F, tile)) {
+            if (F.tile_cost && rtt::lane_id() == 0) F.tile_cost[tile] = 0u;  // still sky: dispatched last again
+            continue;
+        }
+        const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
+        SegClock sg = {0ull, 0ull, 0ull, 0ull};
+        const bool sky = render_tile<false, false, Q4, false, false>(S, F, st, wstack_mem, tile, -1, 4,
+                                                                     threadIdx.x & 63, cnt, sg, p0 + j);
+        if (F.tile_cost && rtt::lane_id() == 0)
+            F.tile_cost[tile] = sky ? 0u : max(1u, tile_cost_key(__builtin_amdgcn_s_memtime() - t0, -1, 4));
+    }
+    rtt::flush_counts<false>(cnt, F.counters);
 }
 
 // Per-wave tallies of a render_kernel launch (F.wave_counts) -> the frame's
@@ -1070,7 +1130,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     static_assert(kMkMinWaves == 6 && W5 == 5, "instance names below");
 #define RT_LAUNCH(K, NAME)                                                                  \
     do {                                                                                    \
-        hipLaunchKernelGGL(K, dim3(blocks), dim3(kMkThreads), 0, stream, S, F);             \
+        if (blocks > 0) hipLaunchKernelGGL(K, dim3(blocks), dim3(kMkThreads), 0, stream, S, F); \
         name = NAME;                                                                        \
     } while (0)
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
@@ -1112,6 +1172,13 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     else
         RT_LAUNCH(render_kernel<false>, "render_kernel<false, false, false, false, 6>");
 #undef RT_LAUNCH
+    if (!count_tests && F.sky_batch_tiles > 0 && F.tile_order && F.max_bounces <= kMaxBounces) {
+        const int sb = (F.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch;
+        if (q4)
+            hipLaunchKernelGGL(sky_batch_kernel<true>, dim3(sb), dim3(kMkThreads), 0, stream, S, F);
+        else
+            hipLaunchKernelGGL(sky_batch_kernel<false>, dim3(sb), dim3(kMkThreads), 0, stream, S, F);
+    }
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
@@ -1121,7 +1188,29 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
 }
 
 int render_mega_waves(const FrameDev &F) {
-    return F.num_tiles <= 0 ? 0 : F.num_tiles + ((64 >> F.s16_shift) - 1) * F.split16_tiles + 3 * F.split_tiles;
+    // (the last F.sky_batch_tiles positions are sky_batch_kernel's; the counting launch's F has none)
+    return F.num_tiles <= 0 ? 0
+                            : F.num_tiles - F.sky_batch_tiles + ((64 >> F.s16_shift) - 1) * F.split16_tiles +
+                                  3 * F.split_tiles;
+}
+
+__global__ __launch_bounds__(256) void sky_count_kernel(const unsigned *sorted, int n, unsigned seq,
+                                                       unsigned long long *out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    // sorted descending: the first 0 key, or n when none (exactly one thread
+    // writes, one 64-bit vector store: the host never sees a torn pair)
+    const bool zero = sorted[i] == 0u;
+    if ((zero && (i == 0 || sorted[i - 1] != 0u)) || (!zero && i == n - 1))
+        __hip_atomic_store(out, ((unsigned long long)seq << 32) | (unsigned)(zero ? i : n), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_sky_count(const unsigned *cost_sorted, int n, unsigned seq, unsigned long long *out,
+                            hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sky_count_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, cost_sorted, n, seq, out);
+    return hipGetLastError();
 }
 
 // Longest-first dispatch for the next frame: tiles sorted by the cost key this
