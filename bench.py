@@ -161,8 +161,8 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     frames only when no frame of another stream runs beside them (lpt_prepare
     overlapped_frame; `in_flight` False: frames one at a time) — Q4 for 2x2
     spp, W the waves per SIMD (5 for shards of <= 70,000 tiles and deep
-    frames, else 6), and a sixth argument `true` for the lone-shard instance
-    whose one-sample waves trace with the whole wave (csrc/coop.h).  The bench's timed frames are in flight (four streams):
+    frames, else 6), SAMPLE (the sixth) for the lone-shard instance whose
+    one-sample waves trace with the whole wave (csrc/coop.h).  The bench's timed frames are in flight (four streams):
     whole frames run the non-split instance."""
     if mode == "packet":
         return "render_packet_kernel<false, true>"
@@ -185,7 +185,7 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     sample = split and not in_flight and spp == 4 and tiles <= 40000
     b = lambda v: "true" if v else "false"  # noqa: E731
     return (f"render_kernel<false, {b(split)}, {b(deep)}, {b(spp == 4 and tw == 4 and th == 4 and not deep)}, "
-            f"{waves}{', true' if sample else ''}>")
+            f"{waves}, {b(sample)}>")
 
 
 def host_facts():

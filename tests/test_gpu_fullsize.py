@@ -5,7 +5,7 @@
   RT_FLAG_ASYNC frames into device buffers (rt_render_device), enough frames
   that longest-first dispatch runs from a measured order and every stream
   has a frame beside it, so the frames run the in-flight instance
-  render_kernel<false, false, false, true, 6> (checked through rt_debug_read
+  render_kernel<false, false, false, true, 6, false> (checked through rt_debug_read
   RT_DEBUG_LAST_LAUNCH).  Every pixel of full 1920x1080 C2 and C3 frames must
   equal, bit for bit, the CPU oracle's walk of the same exported 4-wide tree
   (oracle/rt_oracle.c bvh4_query, itself pinned to the brute-force scan of
@@ -26,8 +26,8 @@ import torch
 
 pytestmark = [pytest.mark.gpu, pytest.mark.fullsize]
 
-IN_FLIGHT = "render_kernel<false, false, false, true, 6>"
-LONE_SPLIT = "render_kernel<false, true, false, true, 6>"
+IN_FLIGHT = "render_kernel<false, false, false, true, 6, false>"
+LONE_SPLIT = "render_kernel<false, true, false, true, 6, false>"
 RAYS = ("primary_rays", "shadow_rays", "reflection_rays")
 
 

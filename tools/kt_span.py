@@ -1,6 +1,6 @@
 """Per-launch device time of one kernel instance from a rocprofv3 kernel trace.
 
-    python tools/kt_span.py gpurun_out/kt_<tag> --kernel "render_kernel<false, false, false, true, 6>"
+    python tools/kt_span.py gpurun_out/kt_<tag> --kernel "render_kernel<false, false, false, true, 6, false>" --with sky_batch_kernel
 
 With frames in flight (bench.py's four streams) the launches of the timed
 instance overlap: each dispatch's own duration (rocprofv3 --stats "average")

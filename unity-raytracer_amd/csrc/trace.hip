@@ -767,8 +767,13 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
 // (wclk_r05s).  A tile that is not sky this frame (the order predates a
 // camera or scene change) is rendered in full, as render_kernel's whole-frame
 // instance would; its tallies go to the counters directly.
+#ifdef RT_EXP_SKYW
+constexpr int kSkyWaves = RT_EXP_SKYW;  // measuring builds only
+#else
+constexpr int kSkyWaves = kMkMinWaves;
+#endif
 template <bool Q4>
-__global__ __launch_bounds__(kMkThreads, kMkMinWaves) void sky_batch_kernel(SceneDev S, FrameDev F) {
+__global__ __launch_bounds__(kMkThreads, kSkyWaves) void sky_batch_kernel(SceneDev S, FrameDev F) {
     __shared__ int stack_mem[kStackSize * kWaveSize];
     __shared__ int wstack_mem[rtp::kWaveStack];
     int ovf[kStackTotal - kStackSize];
@@ -1135,24 +1140,24 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     } while (0)
     if (F.max_bounces > kMaxBounces) {  // mirror chains may outgrow the fold stack
         if (count_tests)
-            RT_LAUNCH((render_kernel<true, false, true, false, W5>), "render_kernel<true, false, true, false, 5>");
+            RT_LAUNCH((render_kernel<true, false, true, false, W5>), "render_kernel<true, false, true, false, 5, false>");
         else
-            RT_LAUNCH((render_kernel<false, false, true, false, W5>), "render_kernel<false, false, true, false, 5>");
+            RT_LAUNCH((render_kernel<false, false, true, false, W5>), "render_kernel<false, false, true, false, 5, false>");
     } else if (count_tests)
-        RT_LAUNCH((render_kernel<true, false, false, false, W5>), "render_kernel<true, false, false, false, 5>");
+        RT_LAUNCH((render_kernel<true, false, false, false, W5>), "render_kernel<true, false, false, false, 5, false>");
     else if (split && q4 && shard && F.s16_shift == 0)
         RT_LAUNCH((render_kernel<false, true, false, true, W5, true>), "render_kernel<false, true, false, true, 5, true>");
     else if (split && q4 && shard)
-        RT_LAUNCH((render_kernel<false, true, false, true, W5>), "render_kernel<false, true, false, true, 5>");
+        RT_LAUNCH((render_kernel<false, true, false, true, W5>), "render_kernel<false, true, false, true, 5, false>");
     else if (split && q4)
-        RT_LAUNCH((render_kernel<false, true, false, true>), "render_kernel<false, true, false, true, 6>");
+        RT_LAUNCH((render_kernel<false, true, false, true>), "render_kernel<false, true, false, true, 6, false>");
     else if (split && shard && F.s16_shift == 0)
         RT_LAUNCH((render_kernel<false, true, false, false, W5, true>),
                   "render_kernel<false, true, false, false, 5, true>");
     else if (split && shard)
-        RT_LAUNCH((render_kernel<false, true, false, false, W5>), "render_kernel<false, true, false, false, 5>");
+        RT_LAUNCH((render_kernel<false, true, false, false, W5>), "render_kernel<false, true, false, false, 5, false>");
     else if (split)
-        RT_LAUNCH((render_kernel<false, true>), "render_kernel<false, true, false, false, 6>");
+        RT_LAUNCH((render_kernel<false, true>), "render_kernel<false, true, false, false, 6, false>");
     else if (S.bvh4 && F.spp >= kLevelsMinSpp) {
         const hipError_t e = launch_render_levels(S, F, stream);
         static const char *const lv[2][3] = {{"render_levels_kernel<6, 8, 4>", "render_levels_kernel<6, 16, 4>",
@@ -1168,9 +1173,9 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         return hipGetLastError();
     }
     else if (q4)
-        RT_LAUNCH((render_kernel<false, false, false, true>), "render_kernel<false, false, false, true, 6>");
+        RT_LAUNCH((render_kernel<false, false, false, true>), "render_kernel<false, false, false, true, 6, false>");
     else
-        RT_LAUNCH(render_kernel<false>, "render_kernel<false, false, false, false, 6>");
+        RT_LAUNCH(render_kernel<false>, "render_kernel<false, false, false, false, 6, false>");
 #undef RT_LAUNCH
     if (!count_tests && F.sky_batch_tiles > 0 && F.tile_order && F.max_bounces <= kMaxBounces) {
         const int sb = (F.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch;
