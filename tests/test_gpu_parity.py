@@ -378,6 +378,16 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res):
         assert np.array_equal(img[1].view(np.uint32), row.view(np.uint32))
         assert np.array_equal(img[0].view(np.uint32), row2.view(np.uint32))
         assert rays(st) == tuple(a + b for a, b in zip(rays(sr), rays(sr2)))
+        # the camera turned away from the scene: every tile is sky; after the
+        # re-sort (each stream's frame 16) the whole order is the sky tail
+        away = rt.CameraData(c.Position, tuple(-v for v in c.Forward), tuple(-v for v in c.Right), c.Up)
+        row3, sr3 = ctx.render(away, fr.plane, prow)
+        for k in range(14):
+            launch, st, img = pair(away)
+            assert np.array_equal(img[0].view(np.uint32), row3.view(np.uint32)), k
+            assert rays(st) == tuple(a + b for a, b in zip(rays(sr), rays(sr3))), k
+        if whole:  # all but one tile (render_kernel keeps a wave)
+            assert int(launch.split("sky=")[1].split()[0]) == int(launch.split("tiles=")[1].split()[0]) - 1, launch
         # a lone frame takes no batches
         ctx.set_stream(None)
         ctx.render(c, fr.plane, rt.frame_params(fr))

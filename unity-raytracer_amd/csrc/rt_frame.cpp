@@ -549,7 +549,8 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // not pixels: a batch renders any tile that is not sky in full).
     if (F.tile_order && !count && !levels && rtk::kSkyBatch > 1 && F.num_tiles > rtk::kShardTilesMax &&
         overlapped_frame(ctx, prm))
-        F.sky_batch_tiles = std::min(ls->sky_tail, F.num_tiles - F.split_tiles - F.split16_tiles);
+        // (render_kernel keeps one wave at least: its launch and tallies stay, an all-sky view included)
+        F.sky_batch_tiles = std::max(0, std::min(ls->sky_tail, F.num_tiles - F.split_tiles - F.split16_tiles - 1));
     {
         char b[128];
         snprintf(b, sizeof b, " lpt: frame=%lld sky_tail=%d known=%d pending=%d overlapped=%d", ls->frames,

@@ -1168,7 +1168,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
                                          : lv[F.spp <= 16 ? 0 : 1][F.max_bounces <= 8 ? 0 : F.max_bounces <= 16 ? 1 : 2];
         if (e != hipSuccess || !F.wave_counts) return e;
         const int waves = F.num_tiles;  // one wave per tile, no splits
-        hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
+        hipLaunchKernelGGL(wave_counts_kernel, dim3(std::max(1, std::min(64, (waves + 1023) / 1024))), dim3(256), 0, stream,
                            (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
         return hipGetLastError();
     }
@@ -1186,7 +1186,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     }
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
-        hipLaunchKernelGGL(wave_counts_kernel, dim3(std::min(64, (waves + 1023) / 1024)), dim3(256), 0, stream,
+        hipLaunchKernelGGL(wave_counts_kernel, dim3(std::max(1, std::min(64, (waves + 1023) / 1024))), dim3(256), 0, stream,
                            (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
     }
     return hipGetLastError();
