@@ -559,10 +559,20 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     }
     if (levels && !(F.max_bounces > rtd::kMaxBounces)) {
         // the levels kernel dispatches XCD-aware stripes in row order
-        // (trace_levels.hip): no longest-first order, no cost measurement
-        F.tile_order = nullptr;
-        F.tile_cost = nullptr;
-        lpt_sort = false;
+        // (trace_levels.hip): no longest-first order.  Its 16-spp instance
+        // (the one with the sky test) measures which tiles are sky, and whole
+        // frames in flight leave those to sky_batch_kernel: its positions are
+        // the non-sky tiles in row order (C4 all-sky frames cost 0.955 ms in
+        // flight as a wave per tile; exp_skycost_r05z).
+        if (F.spp == 16 && rtk::kSkyBatch > 1) {
+            if (F.tile_order && !count && overlapped_frame(ctx, prm))
+                F.sky_batch_tiles = std::max(0, std::min(ls->sky_tail, F.num_tiles - 1));
+            if (F.sky_batch_tiles == 0) F.tile_order = nullptr;  // plain stripes
+        } else {
+            F.tile_order = nullptr;
+            F.tile_cost = nullptr;
+            lpt_sort = false;
+        }
     }
     // render_kernel's ray tallies: one plain store per wave into this slot's
     // buffer, reduced after the launch on the same stream (an atomic per wave

@@ -1166,8 +1166,12 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
                                               "render_levels_kernel<7, 32, 8>"}};
         name = F.spp > 16 && F.spp != 64 ? "render_levels_kernel<7, 32, 0>"
                                          : lv[F.spp <= 16 ? 0 : 1][F.max_bounces <= 8 ? 0 : F.max_bounces <= 16 ? 1 : 2];
-        if (e != hipSuccess || !F.wave_counts) return e;
-        const int waves = F.num_tiles;  // one wave per tile, no splits
+        if (e != hipSuccess) return e;
+        if (F.sky_batch_tiles > 0 && F.tile_order)  // (16 spp in flight: the sky tail of the order)
+            hipLaunchKernelGGL(sky_batch_kernel<false>, dim3((F.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch),
+                               dim3(kMkThreads), 0, stream, S, F);
+        if (!F.wave_counts) return hipGetLastError();
+        const int waves = F.num_tiles - F.sky_batch_tiles;  // one wave per position, no splits
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::max(1, std::min(64, (waves + 1023) / 1024))), dim3(256), 0, stream,
                            (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
         return hipGetLastError();

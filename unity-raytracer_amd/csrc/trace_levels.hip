@@ -119,9 +119,13 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         rk -= zs;
     }
     const int wid = ((int)q * 8 + (blockIdx.x & 7)) * zs + rk;  // the tile itself
-    if (wid >= F.num_tiles) return;  // wave-uniform (the last stripes' padding)
+    // positions: the frame's tiles in row order, or (F.tile_order: whole 16-spp
+    // frames in flight) the last measurement's non-sky tiles in row order — the
+    // sky tail is trace.hip sky_batch_kernel's, and the stripes above keep
+    // their locality over the compacted positions
+    if (wid >= F.num_tiles - F.sky_batch_tiles) return;  // wave-uniform (the last stripes' padding)
     // the tile index in an SGPR (scalar slot -> pixel math, nothing spilled)
-    int tile = __builtin_amdgcn_readfirstlane(wid);
+    int tile = __builtin_amdgcn_readfirstlane(F.tile_order ? rtt::cload(F.tile_order + wid) : wid);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     RT_LSEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
             unsigned long long sg_cam = 0, sg_sh = 0, sg_mir = 0, sg_setup = 0;)
@@ -132,6 +136,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     f3 term = mk(0.0f, 0.0f, 0.0f);
     f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
     bool alive;
+    bool sky_wave = false;  // (the longest-first measurement's key 0: sky_batch_kernel's next time)
     {
         int px, ly, gy, s;
         alive = rts::slot_pixel<FIX>(F, tile, lane, px, ly, gy, s);
@@ -148,6 +153,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
                 rts::primary_ray<FIX>(F, px, gy, s, o, d);
         }
         if (sky) alive = false;
+        sky_wave = sky;
     }
     // The <= 16-spp instance's camera packets start below the top-level cut
     // (packet.h cut_select, as render_kernel's): C4 -5.6 % single frame and
@@ -280,10 +286,10 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
             rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
         }
     }
-    if (F.tile_cost && lane2 == 0) {
+    if (F.tile_cost && lane2 == 0) {  // (16 spp: the sky flag is what the order is for)
         const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
         const unsigned e = c ? 31u - __clz(c) : 0u;
-        F.tile_cost[tile] = e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u));
+        F.tile_cost[tile] = sky_wave ? 0u : max(1u, e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u)));
     }
 #ifdef RT_SEG_PROFILE
     if (lane2 == 0) {  // the clocks are wave-uniform
@@ -319,7 +325,7 @@ hipError_t launch_render_levels(const SceneDev &S, const FrameDev &F0, hipStream
     FrameDev F = F0;
     // whole groups of eight stripes (render_levels_kernel's XCD-aware dispatch)
     const long long rows = F.spp <= 16 ? kXcdStripeRowsLow : kXcdStripeRowsHigh;  // the instance launched below
-    const long long zs = rows * F.tiles_x, ns = (F.num_tiles + zs - 1) / zs;
+    const long long zs = rows * F.tiles_x, ns = (F.num_tiles - F.sky_batch_tiles + zs - 1) / zs;
     F.lv_zs = (int)zs;
     F.lv_zs_magic = zs <= 1 ? 0xffffffffu : (unsigned)((1ull << 32) / (unsigned long long)zs);
     const long long grid = 8 * ((ns + 7) / 8) * zs;
