@@ -1132,7 +1132,9 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     const bool shard = F.num_tiles <= kShardTiles;  // a small frame: its slowest waves set its time
     const bool split = F.split_tiles > 0 || F.split16_tiles > 0;
     constexpr int W5 = kMkMinWavesShard;
+#ifndef RT_EXP_MKWAVES
     static_assert(kMkMinWaves == 6 && W5 == 5, "instance names below");
+#endif
 #define RT_LAUNCH(K, NAME)                                                                  \
     do {                                                                                    \
         if (blocks > 0) hipLaunchKernelGGL(K, dim3(blocks), dim3(kMkThreads), 0, stream, S, F); \
