@@ -102,10 +102,11 @@ def test_timed_path_full_frame_equals_oracle(rt, orc, name):
         torch.cuda.synchronize()
         # every frame with another stream's frame pending beside it runs the in-flight instance
         assert all(l.startswith(IN_FLIGHT) for l in launches[1:]), launches[:6]
-        # ... and C3's (a knot in open space) renders its measured sky tail in
-        # sky_batch_kernel (C2's room has no sky)
+        # ... and renders its measured sky tail in sky_batch_kernel (C3's knot
+        # and C2's open room both fill the centre of the view: 77,616 of the
+        # 129,600 tiles miss the scene box)
         sky = [int(l.split("sky=")[1].split()[0]) for l in launches[1:]]
-        assert all(s > 0 for s in sky) if name == "C3" else not any(sky), launches[:6]
+        assert all(s > 0 for s in sky), launches[:6]
         imgs = [o.cpu().numpy() for o in outs]
         ctx.set_stream(None)
         ref, counts = _walk(orc, fr, ctx)
