@@ -1,5 +1,6 @@
+"""Frames in flight on four streams: the sky tail each launch takes (RT_DEBUG_LAST_LAUNCH; measuring only)."""
 import sys, os
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch, _rt_pkg
 rt = _rt_pkg.load()
 fr = rt.make("C3")

@@ -563,7 +563,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         // (the one with the sky test) measures which tiles are sky, and whole
         // frames in flight leave those to sky_batch_kernel: its positions are
         // the non-sky tiles in row order (C4 all-sky frames cost 0.955 ms in
-        // flight as a wave per tile; exp_skycost_r05z).
+        // flight as a wave per tile; skycost, r05z).
         if (F.spp == 16 && rtk::kSkyBatch > 1) {
             if (F.tile_order && !count && overlapped_frame(ctx, prm))
                 F.sky_batch_tiles = std::max(0, std::min(ls->sky_tail, F.num_tiles - 1));
