@@ -336,7 +336,7 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res, spp):
     """Whole frames in flight (another stream's frame beside them) take the
     last measured order's sky tail kSkyBatch tiles a wave (trace.hip
     sky_batch_kernel, RT_DEBUG_LAST_LAUNCH "sky=N"; lone frames and frames of
-    shard size, <= 70,000 tiles like 480x270, do not; at 16 spp the levels
+    <= 24,000 tiles like 480x270 do not; at 16 spp the levels
     kernel's frames of any size do, its positions then the non-sky tiles).  After
     the camera moves the order is stale until the next re-sort: tiles of that
     tail now show the knot and are rendered in full.  Frames equal row-major
@@ -372,7 +372,7 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res, spp):
             for i in range(2):
                 assert np.array_equal(img[i].view(np.uint32), row.view(np.uint32)), (k, i)
             assert rays(st) == tuple(2 * v for v in rays(sr)), k
-        whole = spp == 16 or (res[0] // 4) * (res[1] // 4) > 70000  # rtk::kShardTilesMax
+        whole = spp == 16 or (res[0] // 4) * (res[1] // 4) > 24000  # rt_frame.cpp kSkyMinTiles
         assert (int(launch.split("sky=")[1].split()[0]) > 0) == whole, launch
         launch, st, img = pair(moved)  # the same (now stale) order, each stream's frame 3 of 16
         assert (int(launch.split("sky=")[1].split()[0]) > 0) == whole, launch

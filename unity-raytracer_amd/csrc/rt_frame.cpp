@@ -297,6 +297,15 @@ constexpr bool kSplitSync = true;
 // profiles/r04/abx_split) — a C3 frame's slowest wave, one tile's mirror chains,
 // ran 0.32 ms against 0.24 ms for all the others (tools/wave_clock.py, r04i);
 // frames in flight on several streams keep the 70,000-tile limit.
+// Sky batches only for frames in flight of more than this many tiles: the
+// batch waves run after the frame's render launch, and a small frame in
+// flight is bound by its own latency (a 1/8 C3 share: +32 %; 1/4 −3.1 %, 1/2
+// −1.5 %, whole frames −4.9 % per frame, r06d).
+#ifdef RT_EXP_SKYMIN
+constexpr int kSkyMinTiles = RT_EXP_SKYMIN;  // measuring builds only
+#else
+constexpr int kSkyMinTiles = 24000;
+#endif
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
 // kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
@@ -543,11 +552,11 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // The sorted order ends with the tiles the last measurement found to be
     // sky (cost key 0, row order): with other frames in flight beside this
     // one, sky_batch_kernel takes them rtk::kSkyBatch a wave after
-    // render_kernel (C3 frames in flight -2.5 %, C2 -4.6 %; a lone frame, whose
-    // critical path the second launch lengthens, +0.5 % C3, +5 % a 1/8 shard:
-    // abx_r05t).  Only the grids depend on this count (a stale one costs time,
+    // render_kernel, together with the launch's tallies (C3 frames in flight
+    // -4.9 % per frame, r06d; a lone frame, whose critical path the batches
+    // lengthen, +0.5 % C3, +5 % a 1/8 shard: abx_r05t).  Only the grids depend on this count (a stale one costs time,
     // not pixels: a batch renders any tile that is not sky in full).
-    if (F.tile_order && !count && !levels && rtk::kSkyBatch > 1 && F.num_tiles > rtk::kShardTilesMax &&
+    if (F.tile_order && !count && !levels && rtk::kSkyBatch > 1 && F.num_tiles > kSkyMinTiles &&
         overlapped_frame(ctx, prm))
         // (render_kernel keeps one wave at least: its launch and tallies stay, an all-sky view included)
         F.sky_batch_tiles = std::max(0, std::min(ls->sky_tail, F.num_tiles - F.split_tiles - F.split16_tiles - 1));

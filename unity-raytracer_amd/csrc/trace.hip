@@ -772,8 +772,42 @@ constexpr int kSkyWaves = RT_EXP_SKYW;  // measuring builds only
 #else
 constexpr int kSkyWaves = kMkMinWaves;
 #endif
+// The tallies of a launch's waves (F.wave_counts, as wave_counts_kernel) by
+// one-wave blocks: block b of nb sums entries b, b + 64 nb, ... lane-strided.
+__device__ __forceinline__ void wave_counts_part(const FrameDev &F, int waves, int b, int nb) {
+    unsigned long long sh = 0, rf = 0, mo = 0;
+    for (int i = b * kWaveSize + (int)(threadIdx.x & 63); i < waves; i += nb * kWaveSize) {
+        const uint4 v = F.wave_counts[i];
+        if (v.w != F.count_tag) continue;
+        sh += v.x;
+        rf += v.y;
+        mo += v.z;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sh += __shfl_xor(sh, off);
+        rf += __shfl_xor(rf, off);
+        mo += __shfl_xor(mo, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        unsigned long long *ctr = F.counters + (size_t)(b % kCounterSlots) * kCounterWords;
+        if (b == 0 && F.primary_total) atomicAdd(ctr + 0, F.primary_total);
+        if (sh) atomicAdd(ctr + 1, sh);
+        if (rf) atomicAdd(ctr + 2, rf);
+        if (mo) atomicAdd(ctr + 8, mo);
+    }
+}
+
+// The work a frame in flight has after its render_kernel / levels launch, in
+// one launch on its stream (a second dependent launch per frame cost a 1/8
+// share in flight 35 %): blocks [0, sky_blocks) the order's sky tail, the
+// rest the launch's per-wave tallies (`waves` entries).
 template <bool Q4>
-__global__ __launch_bounds__(kMkThreads, kSkyWaves) void sky_batch_kernel(SceneDev S, FrameDev F) {
+__global__ __launch_bounds__(kMkThreads, kSkyWaves) void sky_batch_kernel(SceneDev S, FrameDev F, int sky_blocks,
+                                                                          int waves) {
+    if ((int)blockIdx.x >= sky_blocks) {  // wave-uniform
+        wave_counts_part(F, waves, (int)blockIdx.x - sky_blocks, (int)gridDim.x - sky_blocks);
+        return;
+    }
     __shared__ int stack_mem[kStackSize * kWaveSize];
     __shared__ int wstack_mem[rtp::kWaveStack];
     int ovf[kStackTotal - kStackSize];
@@ -1111,6 +1145,10 @@ hipError_t launch_refresh_cut(const BvhNode4 *nodes, CutTable *out, hipStream_t 
 constexpr int kLevelsMinSpp = 16;
 
 
+// one-wave tally blocks of sky_batch_kernel for `waves` entries (as many
+// threads as wave_counts_kernel's up to 64 x 256)
+static int tail_count_blocks(int waves) { return std::max(1, std::min(256, (waves + 255) / 256)); }
+
 hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_tests, hipStream_t stream,
                               const char **instance) {
     const char *dummy = nullptr;
@@ -1169,11 +1207,14 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         name = F.spp > 16 && F.spp != 64 ? "render_levels_kernel<7, 32, 0>"
                                          : lv[F.spp <= 16 ? 0 : 1][F.max_bounces <= 8 ? 0 : F.max_bounces <= 16 ? 1 : 2];
         if (e != hipSuccess) return e;
-        if (F.sky_batch_tiles > 0 && F.tile_order)  // (16 spp in flight: the sky tail of the order)
-            hipLaunchKernelGGL(sky_batch_kernel<false>, dim3((F.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch),
-                               dim3(kMkThreads), 0, stream, S, F);
-        if (!F.wave_counts) return hipGetLastError();
         const int waves = F.num_tiles - F.sky_batch_tiles;  // one wave per position, no splits
+        if (F.sky_batch_tiles > 0 && F.tile_order && F.wave_counts) {  // (16 spp in flight: the order's sky tail)
+            const int sb = (F.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch;
+            hipLaunchKernelGGL(sky_batch_kernel<false>, dim3(sb + tail_count_blocks(waves)), dim3(kMkThreads), 0, stream,
+                               S, F, sb, waves);
+            return hipGetLastError();
+        }
+        if (!F.wave_counts) return hipGetLastError();
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::max(1, std::min(64, (waves + 1023) / 1024))), dim3(256), 0, stream,
                            (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
         return hipGetLastError();
@@ -1183,12 +1224,16 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     else
         RT_LAUNCH(render_kernel<false>, "render_kernel<false, false, false, false, 6, false>");
 #undef RT_LAUNCH
-    if (!count_tests && F.sky_batch_tiles > 0 && F.tile_order && F.max_bounces <= kMaxBounces) {
+    if (!count_tests && F.sky_batch_tiles > 0 && F.tile_order && F.max_bounces <= kMaxBounces && F.wave_counts) {
+        // the order's sky tail and the launch's tallies in one launch
         const int sb = (F.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch;
+        const int waves = render_mega_waves(F);
+        const dim3 g(sb + tail_count_blocks(waves));
         if (q4)
-            hipLaunchKernelGGL(sky_batch_kernel<true>, dim3(sb), dim3(kMkThreads), 0, stream, S, F);
+            hipLaunchKernelGGL(sky_batch_kernel<true>, g, dim3(kMkThreads), 0, stream, S, F, sb, waves);
         else
-            hipLaunchKernelGGL(sky_batch_kernel<false>, dim3(sb), dim3(kMkThreads), 0, stream, S, F);
+            hipLaunchKernelGGL(sky_batch_kernel<false>, g, dim3(kMkThreads), 0, stream, S, F, sb, waves);
+        return hipGetLastError();
     }
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
