@@ -310,11 +310,13 @@ constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hi
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
 // kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
 // a 0.29 ms frame — small slabs first so the copy starts early, then slabs the render keeps ahead
-// of), else kSlabsRenderBound (RGBA8 / RGBA16F: small last slab, little copy after the render);
-// measured best of 9 / 10 weight vectors on C3 (tools/exp/e2e_weights.py, profiles/r03_e2e/).
-// Frames under kSlabMinFrame go in one piece.
+// of); measured best of 9 weight vectors on C3 (tools/exp/e2e_weights.py, profiles/r03_e2e/).
+// Render-bound formats (RGBA8 / RGBA16F: an 8-MB copy against a 0.24-ms frame) go in one piece
+// since round 5: every slab ends in its own slowest tiles, and with the one-sample and whole-frame
+// splits a lone frame's tail is short — RGBA8 0.497 -> 0.472 ms against {1, 2, 2, 1} (and 2 / 3
+// slabs 0.50-0.52; tools/exp/e2e_ab.sh, profiles/r05/r06g/).  Frames under kSlabMinFrame go in
+// one piece too.
 constexpr double kSlabsCopyBound[] = {1, 2, 2, 3, 3, 4};
-constexpr double kSlabsRenderBound[] = {1, 2, 2, 1};
 constexpr size_t kSlabMinFrame = (size_t)2 << 20;
 constexpr int kMaxSlabs = 16;  // slab count range (RT_EXP_SLAB_WEIGHTS measuring builds)
 
@@ -730,10 +732,9 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         double wts[kMaxSlabs];
         for (int k = 0; k < kMaxSlabs; ++k) wts[k] = 1.0;
         const bool copy_bound = F.out_format == rtd::kOutFloat4 || F.out_format == rtd::kOutRGB32F;
-        const double *w0 = copy_bound ? kSlabsCopyBound : kSlabsRenderBound;
-        int nslab = out_bytes < kSlabMinFrame ? 1 : copy_bound ? 6 : 4;
+        int nslab = out_bytes < kSlabMinFrame || !copy_bound ? 1 : 6;
         if (nslab > 1)
-            for (int k = 0; k < nslab; ++k) wts[k] = w0[k];
+            for (int k = 0; k < nslab; ++k) wts[k] = kSlabsCopyBound[k];
 #ifdef RT_EXP_SLAB_WEIGHTS
         {  // measuring builds: -DRT_EXP_SLAB_WEIGHTS=1,1,2,4,8 (relative slab rows)
             constexpr double w[] = {RT_EXP_SLAB_WEIGHTS};
