@@ -320,7 +320,11 @@ constexpr int kMkMinWaves = RT_EXP_MKWAVES;  // measuring builds only
 #else
 constexpr int kMkMinWaves = 6;
 #endif
+#ifdef RT_EXP_MKWSHARD
+constexpr int kMkMinWavesShard = RT_EXP_MKWSHARD;  // measuring builds only
+#else
 constexpr int kMkMinWavesShard = 5;
+#endif
 // LDS stack entries of the 5-wave instances: 24 (a 1/2 C3 shard, single frame:
 // 0.199 ms with 16 entries, 0.186 with 24, r04i; the LDS does not bind at five waves)
 constexpr int kStackShard = 24;
@@ -1170,7 +1174,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
     const bool shard = F.num_tiles <= kShardTiles;  // a small frame: its slowest waves set its time
     const bool split = F.split_tiles > 0 || F.split16_tiles > 0;
     constexpr int W5 = kMkMinWavesShard;
-#ifndef RT_EXP_MKWAVES
+#if !defined(RT_EXP_MKWAVES) && !defined(RT_EXP_MKWSHARD)
     static_assert(kMkMinWaves == 6 && W5 == 5, "instance names below");
 #endif
 #define RT_LAUNCH(K, NAME)                                                                  \
