@@ -180,7 +180,8 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     tw = ppw // th
     tiles = -(-res_x // tw) * -(-local_rows // th)
     split = not deep and ((16 % spp == 0 and tiles <= 24000) or (4 % spp == 0 and (tiles <= 70000 or not in_flight)))
-    waves = 5 if deep or (split and tiles <= 70000) else 6
+    # (in flight, shards of more than 24,000 tiles take the 6-wave split instance)
+    waves = 5 if deep or (split and tiles <= 70000 and not (in_flight and tiles > 24000)) else 6
     # a lone shard of <= 40,000 tiles at 4 spp: one-sample waves, the SAMPLE instance
     sample = split and not in_flight and spp == 4 and tiles <= 40000
     b = lambda v: "true" if v else "false"  # noqa: E731

@@ -397,6 +397,44 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res, spp):
         ctx.set_stream(None)
 
 
+@pytest.mark.parametrize("band", [(1, 4), (0, 2), (5, 8)])
+def test_shares_in_flight_equal_row_major(gpu_ctx, rt, band):
+    """One rank's share of a C3 frame, frames in flight on two streams (the
+    bench's --sim-bands case): shares of more than 24,000 tiles (1/2, 1/4)
+    take the 6-wave split instance and sky batches, a 1/8 share the 5-wave
+    one — every frame equals the row-major share frame bit for bit."""
+    import torch
+    fr = rt.make("C3")
+    ctx = gpu_ctx
+    ctx.set_scene(fr.scene)
+    bi, bn = band
+    kw = dict(band_index=bi, band_count=bn, band_rows=8)
+    row, sr = ctx.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
+    outs = [torch.empty(row.shape, dtype=torch.float32, device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    pa = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC, **kw)
+    try:
+        launches = []
+        for f in range(12):
+            k = f % 2
+            ctx.set_stream(streams[k].cuda_stream)
+            ctx.render_device(fr.camera, fr.plane, pa, outs[k].data_ptr(), outs[k].numel() * 4)
+            launches.append(ctx.last_launch())
+            if k == 1:
+                st = ctx.finish()
+                torch.cuda.synchronize()
+                for i in range(2):
+                    assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), row.view(np.uint32)), (f, i)
+                assert (st.primary_rays, st.shadow_rays, st.reflection_rays) == tuple(
+                    2 * v for v in (sr.primary_rays, sr.shadow_rays, sr.reflection_rays)), f
+        tiles = int(launches[-1].split("tiles=")[1].split()[0])
+        w = 6 if tiles > 24000 else 5
+        assert launches[-1].startswith(f"render_kernel<false, true, false, true, {w}, false>"), launches[-1]
+        assert (int(launches[-1].split("sky=")[1].split()[0]) > 0) == (tiles > 24000), launches[-1]
+    finally:
+        ctx.set_stream(None)
+
+
 @pytest.mark.parametrize("name", ["C1", "C2", "C3", "C5"])
 @pytest.mark.parametrize("cap", [0, 40, 1])
 def test_one_sample_waves_trace_with_the_whole_wave(gpu_ctx, rt, name, cap):

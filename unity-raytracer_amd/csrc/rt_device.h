@@ -274,6 +274,7 @@ struct FrameDev {
     // wave's LDS stack area allows (testing knob: a small value makes every
     // step depth-first, rt_debug_set)
     int sample_wave_stack;
+    int in_flight;  // 1: other frames of the context are in flight beside this one (rt_frame.cpp overlapped_frame)
     // measuring builds only (RT_EXP_PERSIST): a whole frame's non-split launch
     // as persist_waves resident waves pulling longest-first tiles from eight
     // per-XCD tile counters (persist_ctr, 16 ints apart, zeroed per launch)

@@ -450,6 +450,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
                 ls->stream = ctx->stream;
                 ls->slab = slab;
             }
+    F.in_flight = overlapped_frame(ctx, prm) ? 1 : 0;
     if (!ls) return RT_OK;  // more (stream, slab) pairs than slots: row-major order
     const long long key = ((long long)F.num_tiles << 32) ^ ((long long)F.tiles_x << 20) ^ ((long long)F.spp << 12) ^
                           ((long long)F.band_count << 6) ^ F.band_index ^ ((long long)F.row0 << 44);

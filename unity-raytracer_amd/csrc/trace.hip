@@ -334,6 +334,14 @@ constexpr int kStackShard = 24;
 // F.split_samples and the last to arrive sums them (render_tile).
 __device__ __forceinline__ int s16_shift(const FrameDev &F) { return __builtin_amdgcn_readfirstlane(F.s16_shift); }
 constexpr int kShardTiles = rtk::kShardTilesMax;  // a 1/2 shard of 1080p at 4 spp
+// ... but a shard of more tiles than this with other frames in flight beside
+// it takes the 6-wave split instance: a 1/4 C3 share in flight -11.4 % per
+// frame (0.0812 -> 0.0719 ms), a 1/8 share +8 %, lone shards +7 to +21 % (r06j)
+#ifdef RT_EXP_SHARDW6
+constexpr int kShardW6InFlight = RT_EXP_SHARDW6;  // measuring builds only
+#else
+constexpr int kShardW6InFlight = 24000;
+#endif
 // Waves per megakernel workgroup.  A workgroup's slot is recycled only when
 // all of its waves are done, and path lengths vary a lot between tiles, so
 // small workgroups keep the CUs fuller near the end of each wave "round".
@@ -1171,7 +1179,8 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         F.persist_waves = 0;
 #endif
     const bool q4 = F.spp == 4 && F.tile_w == 4 && F.tile_h == 4;
-    const bool shard = F.num_tiles <= kShardTiles;  // a small frame: its slowest waves set its time
+    // a small frame: its slowest waves set its time (unless frames in flight hide them)
+    const bool shard = F.num_tiles <= kShardTiles && !(F.in_flight && F.num_tiles > kShardW6InFlight);
     const bool split = F.split_tiles > 0 || F.split16_tiles > 0;
     constexpr int W5 = kMkMinWavesShard;
 #if !defined(RT_EXP_MKWAVES) && !defined(RT_EXP_MKWSHARD)
