@@ -343,7 +343,7 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res, spp):
     frames bit for bit, with the same ray counts, before and after the move."""
     import torch
     fr = rt.make("C3").with_resolution(*res).with_(spp=spp)
-    ctx = gpu_ctx
+    ctx = rt.Context()  # its own (stream, slab) longest-first slots
     ctx.set_scene(fr.scene)
     c = fr.camera
     moved = rt.CameraData(tuple(float(a + 1.5 * b) for a, b in zip(c.Position, c.Right)), c.Forward, c.Right, c.Up)
@@ -395,6 +395,7 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res, spp):
         assert "sky=0" in ctx.last_launch(), ctx.last_launch()
     finally:
         ctx.set_stream(None)
+        ctx.close()
 
 
 @pytest.mark.parametrize("band", [(1, 4), (0, 2), (5, 8)])
@@ -405,7 +406,9 @@ def test_shares_in_flight_equal_row_major(gpu_ctx, rt, band):
     one — every frame equals the row-major share frame bit for bit."""
     import torch
     fr = rt.make("C3")
-    ctx = gpu_ctx
+    # a context of its own: a context keeps longest-first state for 16
+    # (stream, slab) pairs, and the shared one has met many streams by now
+    ctx = rt.Context()
     ctx.set_scene(fr.scene)
     bi, bn = band
     kw = dict(band_index=bi, band_count=bn, band_rows=8)
@@ -433,6 +436,7 @@ def test_shares_in_flight_equal_row_major(gpu_ctx, rt, band):
         assert (int(launches[-1].split("sky=")[1].split()[0]) > 0) == (tiles > 24000), launches[-1]
     finally:
         ctx.set_stream(None)
+        ctx.close()
 
 
 @pytest.mark.parametrize("name", ["C1", "C2", "C3", "C5"])

@@ -336,7 +336,8 @@ __device__ __forceinline__ int s16_shift(const FrameDev &F) { return __builtin_a
 constexpr int kShardTiles = rtk::kShardTilesMax;  // a 1/2 shard of 1080p at 4 spp
 // ... but a shard of more tiles than this with other frames in flight beside
 // it takes the 6-wave split instance: a 1/4 C3 share in flight -11.4 % per
-// frame (0.0812 -> 0.0719 ms), a 1/8 share +8 %, lone shards +7 to +21 % (r06j)
+// frame (0.0812 -> 0.0719 ms), a 1/8 share +8 %, lone shards +7 to +21 % (r06j);
+// then (r06k) 1/2 -13.6 %, 1/4 -9.8 %, 1/8 +-0
 #ifdef RT_EXP_SHARDW6
 constexpr int kShardW6InFlight = RT_EXP_SHARDW6;  // measuring builds only
 #else
