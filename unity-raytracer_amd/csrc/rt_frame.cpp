@@ -230,7 +230,11 @@ constexpr int kSplit16Div = RT_EXP_SPLIT16DIV;  // measuring builds only
 #else
 constexpr int kSplit16Div = 2048;  // of those, 1/kSplit16Div of the tiles as sixteenth-waves; 0: off
 #endif
+#ifdef RT_EXP_SPLITDIV
+constexpr int kSplitDiv = RT_EXP_SPLITDIV;  // measuring builds only
+#else
 constexpr int kSplitDiv = 256;  // 1/kSplitDiv of the tiles (the slowest) run as quarter-waves; 0: off
+#endif
 // A lone shard's finely split tiles run as one-sample waves traced by the
 // whole wave (trace.hip render_sample_wave, csrc/coop.h): cheap enough to
 // split its slowest 1/256 so (1/1024 before the whole-wave traversal: the
