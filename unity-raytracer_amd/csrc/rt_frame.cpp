@@ -310,6 +310,12 @@ constexpr int kSkyMinTiles = RT_EXP_SKYMIN;  // measuring builds only
 #else
 constexpr int kSkyMinTiles = 24000;
 #endif
+// Lone whole frames take sky batches too (measuring builds: -DRT_EXP_SKYLONE=1)
+#ifdef RT_EXP_SKYLONE
+constexpr bool kSkyLone = RT_EXP_SKYLONE != 0;
+#else
+constexpr bool kSkyLone = false;
+#endif
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
 // kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
@@ -564,7 +570,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // lengthen, +0.5 % C3, +5 % a 1/8 shard: abx_r05t).  Only the grids depend on this count (a stale one costs time,
     // not pixels: a batch renders any tile that is not sky in full).
     if (F.tile_order && !count && !levels && rtk::kSkyBatch > 1 && F.num_tiles > kSkyMinTiles &&
-        overlapped_frame(ctx, prm))
+        (overlapped_frame(ctx, prm) || (kSkyLone && F.num_tiles > rtk::kShardTilesMax)))
         // (render_kernel keeps one wave at least: its launch and tallies stay, an all-sky view included)
         F.sky_batch_tiles = std::max(0, std::min(ls->sky_tail, F.num_tiles - F.split_tiles - F.split16_tiles - 1));
     {
