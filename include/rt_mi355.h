@@ -157,7 +157,9 @@ typedef struct rt_render_params {
  * with rt_set_stream between frames lets consecutive frames overlap).  The
  * stats argument is zeroed; rt_finish waits for the device and returns the
  * counters and device time of all asynchronous frames since the previous
- * rt_finish. */
+ * rt_finish.  The first frame of a (stream, layout) waits once for the
+ * device after its launch: its measured longest-first order's sky tail is
+ * read back (frames in flight beside it render that tail in batches). */
 #define RT_FLAG_ASYNC       32
 /* Megakernel frames normally dispatch their tiles longest-first, ordered by
  * the per-tile cost an earlier frame of the same layout and scene measured on
