@@ -316,7 +316,11 @@ constexpr bool kSkyLone = RT_EXP_SKYLONE != 0;
 #else
 constexpr bool kSkyLone = false;
 #endif
+#ifdef RT_EXP_LPTPERIOD
+constexpr int kLptPeriod = RT_EXP_LPTPERIOD;  // measuring builds only
+#else
 constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
+#endif
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
 // kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
 // a 0.29 ms frame — small slabs first so the copy starts early, then slabs the render keeps ahead
