@@ -93,7 +93,7 @@ def test_timed_path_full_frame_equals_oracle(rt, orc, name):
         ctx.finish()
         torch.cuda.synchronize()
         frames, launches = 36, []
-        for f in range(frames):  # > 16 per stream... and past a longest-first re-sort on every stream
+        for f in range(frames):  # nine per stream, each stream's order measured by its setup frame
             k = f % len(streams)
             ctx.set_stream(streams[k].cuda_stream)
             ctx.render_device(cam, pl, p, outs[k].data_ptr(), nbytes)

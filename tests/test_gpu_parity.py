@@ -374,16 +374,17 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res, spp):
             assert rays(st) == tuple(2 * v for v in rays(sr)), k
         whole = spp == 16 or (res[0] // 4) * (res[1] // 4) > 24000  # rt_frame.cpp kSkyMinTiles
         assert (int(launch.split("sky=")[1].split()[0]) > 0) == whole, launch
-        launch, st, img = pair(moved)  # the same (now stale) order, each stream's frame 3 of 16
+        launch, st, img = pair(moved)  # the same (now stale) order, each stream's frame 3 of 32
         assert (int(launch.split("sky=")[1].split()[0]) > 0) == whole, launch
         assert np.array_equal(img[1].view(np.uint32), row.view(np.uint32))
         assert np.array_equal(img[0].view(np.uint32), row2.view(np.uint32))
         assert rays(st) == tuple(a + b for a, b in zip(rays(sr), rays(sr2)))
         # the camera turned away from the scene: every tile is sky; after the
-        # re-sort (each stream's frame 16) the whole order is the sky tail
+        # re-sort (each stream's frame 32, rt_frame.cpp kLptPeriod) the whole
+        # order is the sky tail
         away = rt.CameraData(c.Position, tuple(-v for v in c.Forward), tuple(-v for v in c.Right), c.Up)
         row3, sr3 = ctx.render(away, fr.plane, prow)
-        for k in range(14):
+        for k in range(30):
             launch, st, img = pair(away)
             assert np.array_equal(img[0].view(np.uint32), row3.view(np.uint32)), k
             assert rays(st) == tuple(a + b for a, b in zip(rays(sr), rays(sr3))), k

@@ -319,7 +319,10 @@ constexpr bool kSkyLone = false;
 #ifdef RT_EXP_LPTPERIOD
 constexpr int kLptPeriod = RT_EXP_LPTPERIOD;  // measuring builds only
 #else
-constexpr int kLptPeriod = 16;  // frames between longest-first re-sorts (one hipCUB sort ~46 us)
+// frames between longest-first re-sorts (one hipCUB sort ~46 us, plus the
+// measuring launch's clock reads): 32 since round 5 (C3 in flight +1.9 %
+// against 16, 64 +0.4 %: r06p)
+constexpr int kLptPeriod = 32;
 #endif
 // rt_render's host-output pipeline: row slabs alternating over two streams, relative row counts
 // kSlabsCopyBound when the PCIe copy is the longer part (float RGBA: 33 MB at 1080p, 0.59 ms against
