@@ -356,6 +356,10 @@ def main():
                          "tiles overlap the next frame's bulk (1 = one frame at a time)")
     ap.add_argument("--gather-frames", type=int, default=0,
                     help="N > 1: frames per RCCL gather (one collective per group of frames; 0 = --streams)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per launch (rt_render_device_batch: frames of one layout from their own cameras as "
+                         "one launch, their tiles under one longest-first order); 0 = 4 for a rank's row band "
+                         "(N > 1 or --sim-bands: each band alone is too small to fill the GPU), 1 otherwise")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--sim-bands", type=int, default=0,
                     help="experiment (one GPU, no gather): render only row band 0 of N, i.e. one rank's share "
@@ -442,11 +446,17 @@ def main():
     # host time) below a 1/8 shard's frame time.
     nstreams = max(1, args.streams)
     streams = [stream] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
+    # Batches (a rank's row band, N > 1 or --sim-bands): the frames of a group
+    # go as ONE launch (rt_render_device_batch) into the group's buffer, the
+    # groups alternate over two streams (two batches in flight); one
+    # collective per group as before.
+    batch = args.batch or (4 if (dist_on or args.sim_bands) and band_count > 1 else 1)
+    batch = max(1, min(batch, rt.abi.RT_MAX_BATCH))
     # sharded frames travel as float RGB (RT_FLAG_OUT_RGB32F: the Color values
     # bit for bit without the constant alpha, 12 B/px): a quarter less to gather
     ch = 3 if dist_on else 4
-    G = (args.gather_frames or nstreams) if dist_on else 1
-    ngroups = 2 if dist_on else max(1, -(-nstreams // G))
+    G = batch if batch > 1 else ((args.gather_frames or nstreams) if dist_on else 1)
+    ngroups = 2 if dist_on or batch > 1 else max(1, -(-nstreams // G))
     groups = [torch.empty((G, local_rows, rx, ch), dtype=torch.float32, device="cuda") for _ in range(ngroups)]
     nbuf = G * ngroups
     outs = [groups[b // G][b % G] for b in range(nbuf)]
@@ -514,7 +524,36 @@ def main():
                 sb.wait_stream(streams[(used - 2 - k) % nstreams])
             begin_gather(g)
 
+    batch_cams = []
+    batch_no = [0]
+
+    def flush_batch():
+        """The pending frames of the current group as one launch on the
+        group's stream (after the group's previous gather is done), then
+        the group's gather."""
+        if not batch_cams:
+            return
+        g = batch_no[0] % ngroups
+        sb = streams[g % nstreams]
+        ctx.set_stream(sb.cuda_stream)
+        if dist_on:
+            with torch.cuda.stream(sb):  # RCCL's wait targets the current stream
+                finish_gather(g)
+        ctx.render_device_batch(list(batch_cams), plane_s, aparams, groups[g].data_ptr(), nbytes)
+        if dist_on:
+            with torch.cuda.stream(sb):
+                begin_gather(g)
+        batch_cams.clear()
+        batch_no[0] += 1
+
     def step(cam=None):
+        if batch > 1:
+            last_frame[0] = frame_no[0]
+            batch_cams.append(cam or cam_s)
+            frame_no[0] += 1
+            if len(batch_cams) == G:
+                flush_batch()
+            return
         f = frame_no[0]
         b = f % nbuf
         g, j = b // G, b % G
@@ -534,6 +573,17 @@ def main():
         frame_no[0] += 1
 
     def drain():
+        if batch > 1:
+            if batch_cams:  # a partial group: its frames as one launch, the next frame starts a fresh group
+                frame_no[0] += G - len(batch_cams)
+                flush_batch()
+            if dist_on:
+                for k in range(ngroups):
+                    with torch.cuda.stream(stream):
+                        ctx.set_stream(stream.cuda_stream)
+                        finish_gather(k)
+            ctx.set_stream(stream.cuda_stream)
+            return
         if dist_on:
             j = frame_no[0] % G
             if j:  # a partial group: gather it as is and start the next frame on a fresh group
@@ -561,9 +611,14 @@ def main():
     # milliseconds; with W < --streams that setup would otherwise land in
     # the timed region (measured: 0.29 ms of host stall per timed frame at
     # K = 20, W = 3).
-    for sb in streams:
-        ctx.set_stream(sb.cuda_stream)
-        ctx.render_device(cam_s, plane_s, aparams, out.data_ptr(), nbytes)
+    if batch > 1:  # a batch on each group's stream: the batch slots' longest-first state
+        for _ in range(ngroups * G):
+            step()
+        drain()
+    else:
+        for sb in streams:
+            ctx.set_stream(sb.cuda_stream)
+            ctx.render_device(cam_s, plane_s, aparams, out.data_ptr(), nbytes)
     ctx.finish()
     torch.cuda.synchronize()
     for _ in range(args.warmup):
@@ -698,6 +753,10 @@ def main():
         avg_kernel_s = kernel_ms / args.steps / 1e3  # rank 0's timed frames, HIP events
         pmc, pmc_state = load_pmc(args.config, lib_path, band_count)
         kname = trace_kernel_name(args.mode, fr.spp, fr.max_bounces, rx, local_rows, in_flight=nstreams > 1)
+        if batch > 1 and timed_launch.startswith("render_batch_kernel"):
+            # one launch renders `batch` frames: per-launch counters are not per-frame figures
+            kname = timed_launch.split()[0]
+            pmc, pmc_state = None, f"not measured for batch launches ({batch} frames a launch)"
         rays_per_frame = rays // args.steps
         line = {
             "metric": METRIC,
@@ -732,10 +791,11 @@ def main():
                 # behind the surface): counted above, not traversed
                 "shadow_rays_moot": moot // args.steps,
                 "mrays_per_s_traversed": (rays - moot) / elapsed / 1e6,
-                "frames_in_flight": nstreams,
+                "frames_in_flight": batch * min(ngroups, nstreams) if batch > 1 else nstreams,
                 "timed_launch": timed_launch,
                 "lone_launch": lone_launch,
                 "frames_per_gather": G if dist_on else None,
+                "frames_per_launch": batch,
                 # device time per timed frame (HIP events over the timed frames)
                 "kernel_ms_per_frame": kernel_ms_max / args.steps,
                 # one frame at a time (the split instance of a lone frame)
@@ -753,7 +813,8 @@ def main():
             "roofline": {**roofline(pmc, pmc_state, kname, avg_kernel_s, logical), "canonical_counts": canonical,
                          # whole frames in flight: the order's sky tail in a second launch per frame
                          # (trace.hip sky_batch_kernel); avg_kernel_ms and the counters cover both
-                         **({"with": f"sky_batch_kernel<{'true' if fr.spp == 4 else 'false'}>",
+                         **({"with": "sky_batch_batch_kernel" if batch > 1 else
+                             f"sky_batch_kernel<{'true' if fr.spp == 4 else 'false'}>",
                              "with_tiles": sky_tiles} if sky_tiles else {})},
         }
         if world == 1 and not args.no_cpu_baseline:

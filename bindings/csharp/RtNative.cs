@@ -181,6 +181,11 @@ namespace RayTracer.Native
                                                                   ref RtImagePlane plane, ref RtRenderParams p,
                                                                   IntPtr devicePixels, UIntPtr outBytes,
                                                                   out RtStats stats);
+        // frames in flight of one layout from their own cameras as one launch (device outputs back to back)
+        [DllImport(Lib)] public static extern int rt_render_device_batch(IntPtr ctx, int numFrames,
+                                                                        [In] CameraData[] cams, ref RtImagePlane plane,
+                                                                        ref RtRenderParams p, IntPtr devicePixels,
+                                                                        UIntPtr frameStrideBytes, out RtStats stats);
         [DllImport(Lib)] public static extern int rt_band_rows_local(int resolutionY, int bandIndex, int bandCount,
                                                                     int bandRows);
         [DllImport(Lib)] public static extern int rt_assemble_bands(IntPtr ctx, IntPtr gathered, int resolutionX,

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum rt_status {
@@ -391,6 +391,25 @@ int32_t rt_pixel_bytes(int32_t flags);
 int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
                      const rt_render_params *params, void *d_out_rgba, size_t out_bytes,
                      rt_stats *stats);
+
+/* Up to RT_MAX_BATCH frames of one layout (plane, params) from their own
+ * cameras, as one device launch: the throughput path for frames in flight
+ * whose frames are small — e.g. the frames of one gather group of a rank's
+ * row band (band_count > 1), each far too small to fill the GPU alone.  Frame
+ * i is rendered exactly as rt_render_device(cameras[i]) would render it (same
+ * bits, same ray counts; the stats are summed) into the device buffer at
+ * d_out + i * frame_stride_bytes (frame_stride_bytes >= one frame's bytes).
+ * The frames' tiles form one longest-first order, so one frame's slowest tiles
+ * overlap the others' work.  RT_FLAG_ASYNC as for rt_render_device.  Frames
+ * the batch launch does not cover (other than 4 spp, MaxReflectionBounces >
+ * 32, RT_FLAG_COUNT_TESTS / _WAVEFRONT / _PACKET, multi-device contexts) are
+ * rendered one by one with the same results.  No reference counterpart:
+ * RayTracingSetup.Update (RayTracingSetup.cs:171-199) renders one frame per
+ * call. */
+#define RT_MAX_BATCH 8
+int rt_render_device_batch(rt_ctx *ctx, int32_t num_frames, const rt_camera *cameras,
+                           const rt_image_plane *plane, const rt_render_params *params, void *d_out,
+                           size_t frame_stride_bytes, rt_stats *stats);
 
 /* Rows of the compact per-shard buffer for (resolution_y, band_index,
  * band_count, band_rows). */

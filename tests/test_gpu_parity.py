@@ -399,6 +399,126 @@ def test_sky_batches_render_tiles_that_stopped_being_sky(gpu_ctx, rt, res, spp):
         ctx.close()
 
 
+def test_sky_count_waits_only_for_frames_that_use_it(gpu_ctx, rt):
+    """A longest-first slot's first sort makes the host wait for its sky-tail
+    count only when a frame like it takes sky batches (frames in flight of more
+    than 24,000 tiles, rt_frame.cpp sky_tail_usable).  RT_FLAG_ASYNC frames that
+    alternate two layouts on one stream re-sort at every layout change and are
+    lone frames: no wait (RT_DEBUG_LAST_LAUNCH sky_waits), same bits as
+    row-major frames.  Whole frames in flight on two streams do wait, once per
+    slot."""
+    import torch
+    base = rt.make("C3")
+    frs = [base.with_resolution(960, 540), base.with_resolution(1920, 1080)]
+    ctx = rt.Context()
+    ctx.set_scene(base.scene)
+    waits = lambda: int(ctx.last_launch().split("sky_waits=")[1].split()[0])  # noqa: E731
+    try:
+        rows = [ctx.render(f.camera, f.plane, rt.frame_params(f, flags=rt.abi.RT_FLAG_ROW_ORDER))[0] for f in frs]
+        outs = [torch.empty(r.shape, dtype=torch.float32, device="cuda") for r in rows]
+        s = torch.cuda.Stream()
+        ctx.set_stream(s.cuda_stream)
+        for k in range(7):
+            i = k % 2
+            f = frs[i]
+            ctx.render_device(f.camera, f.plane, rt.frame_params(f, flags=rt.abi.RT_FLAG_ASYNC), outs[i].data_ptr(),
+                              outs[i].numel() * 4)
+            assert waits() == 0, (k, ctx.last_launch())
+            ctx.finish()
+            torch.cuda.synchronize()
+            assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), rows[i].view(np.uint32)), k
+        # whole 1080p frames in flight: the first sort of each stream's slot waits once
+        streams = [s, torch.cuda.Stream()]
+        f = frs[1]
+        for k in range(6):
+            ctx.set_stream(streams[k % 2].cuda_stream)
+            ctx.render_device(f.camera, f.plane, rt.frame_params(f, flags=rt.abi.RT_FLAG_ASYNC), outs[1].data_ptr(),
+                              outs[1].numel() * 4)
+        ctx.finish()
+        torch.cuda.synchronize()
+        assert 1 <= waits() <= 2, ctx.last_launch()
+    finally:
+        ctx.set_stream(None)
+        ctx.close()
+
+
+@pytest.mark.parametrize("name,res,band", [("C3", None, (5, 8)), ("C3", None, (0, 8)), ("C3", (480, 270), None),
+                                           ("C2", None, (3, 8)), ("C5", (960, 540), (1, 4))])
+def test_batches_equal_single_frames(gpu_ctx, rt, name, res, band):
+    """rt_render_device_batch: frames of one layout from their own cameras as
+    one launch (trace.hip render_batch_kernel; the batch's tiles under one
+    longest-first order, its sky tail in sky_batch_batch_kernel) — every frame
+    bit-identical to the row-major single frame of its camera, ray counts the
+    sum.  Two batches in flight on two streams, then lone batches; the cameras
+    change between batches, so a batch's sky tail (measured on other cameras)
+    holds tiles that are no longer sky (rendered by the out-of-line per-lane
+    path) and its splits fall on other tiles."""
+    import torch
+    fr = rt.make(name)
+    if res:
+        fr = fr.with_resolution(*res)
+    fr = fr.with_(spp=4)
+    ctx = rt.Context()
+    ctx.set_scene(fr.scene)
+    kw = dict(band_index=band[0], band_count=band[1], band_rows=8) if band else {}
+    c = fr.camera
+    cams = [c] + [rt.CameraData(tuple(float(a + k * 0.35 * b) for a, b in zip(c.Position, c.Right)), c.Forward, c.Right,
+                                c.Up) for k in (1, 2, -1)]
+    prow = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw)
+    refs, rst = [], []
+    for cam in cams:
+        img, st = ctx.render(cam, fr.plane, prow)
+        refs.append(img)
+        rst.append((st.primary_rays, st.shadow_rays, st.reflection_rays))
+    shape = refs[0].shape
+    fb = int(np.prod(shape)) * 4
+    bufs = [torch.empty((4,) + shape, dtype=torch.float32, device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    pa = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC, **kw)
+    rays = lambda s: (s.primary_rays, s.shadow_rays, s.reflection_rays)  # noqa: E731
+    # (batch cameras) per step: equal, then mixed, then moved, then 3-frame batches
+    plan = [[0, 0, 0, 0]] * 3 + [[0, 1, 2, 3]] * 2 + [[3, 2, 1, 0]] + [[1, 1, 2]] * 2
+    try:
+        for k, sel in enumerate(plan):
+            for lone in (False, True):
+                n = 2 if not lone else 1  # two batches in flight, then one at a time
+                for i in range(n):
+                    ctx.set_stream(streams[i].cuda_stream)
+                    ctx.render_device_batch([cams[j] for j in sel], fr.plane, pa, bufs[i].data_ptr(), fb)
+                launch = ctx.last_launch()
+                st = ctx.finish()
+                torch.cuda.synchronize()
+                assert launch.startswith("render_batch_kernel<"), launch
+                assert f"frames={len(sel)}" in launch, launch
+                for i in range(n):
+                    got = bufs[i].cpu().numpy()
+                    for f, j in enumerate(sel):
+                        assert np.array_equal(got[f].view(np.uint32), refs[j].view(np.uint32)), (k, lone, i, f, launch)
+                want = tuple(n * sum(rst[j][q] for j in sel) for q in range(3))
+                assert rays(st) == want, (k, lone, launch)
+    finally:
+        ctx.set_stream(None)
+        ctx.close()
+
+
+def test_batch_falls_back_to_single_frames(gpu_ctx, rt):
+    """Frames a batch launch does not cover (here 1 spp and 16 spp) are
+    rendered one by one by rt_render_device_batch: same bits and counts."""
+    import torch
+    for spp in (1, 16):
+        fr = rt.make("C3").with_resolution(160, 90).with_(spp=spp)
+        gpu_ctx.set_scene(fr.scene)
+        ref, sr = gpu_ctx.render(fr.camera, fr.plane, rt.frame_params(fr))
+        fb = ref.size * 4
+        buf = torch.empty((3,) + ref.shape, dtype=torch.float32, device="cuda")
+        st = gpu_ctx.render_device_batch([fr.camera] * 3, fr.plane, rt.frame_params(fr), buf.data_ptr(), fb)
+        got = buf.cpu().numpy()
+        for f in range(3):
+            assert np.array_equal(got[f].view(np.uint32), ref.view(np.uint32)), (spp, f)
+        assert (st.primary_rays, st.shadow_rays) == (3 * sr.primary_rays, 3 * sr.shadow_rays), spp
+        assert not gpu_ctx.last_launch().startswith("render_batch_kernel"), gpu_ctx.last_launch()
+
+
 @pytest.mark.parametrize("band", [(1, 4), (0, 2), (5, 8)])
 def test_shares_in_flight_equal_row_major(gpu_ctx, rt, band):
     """One rank's share of a C3 frame, frames in flight on two streams (the

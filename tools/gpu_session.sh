@@ -63,6 +63,24 @@ if has bench; then
   timeout -k 10 300 python bench.py > $out/bench_$tag.log 2>&1 || fail bench $out/bench_$tag.log
   tail -1 $out/bench_$tag.log
 fi
+if has drv; then
+  # the driver's own command (BENCH_rNN.json "cmd"), twice, its rocprofv3 kernel
+  # trace (the timed window's fill / drain / per-frame spans: tools/kt_window.py),
+  # and a 200-frame line for the window comparison
+  for k in 1 2; do
+    timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $out/drv${k}_$tag.log 2>&1 \
+      || fail drv$k $out/drv${k}_$tag.log
+    tail -1 $out/drv${k}_$tag.log | cut -c1-400
+  done
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/ktdrv_$tag -o run --output-format csv -- \
+    python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $R/$out/ktdrv_$tag.log 2>&1 \
+    || fail ktdrv $R/$out/ktdrv_$tag.log
+  cd $R
+  timeout -k 10 300 python3 bench.py --steps 200 --warmup 10 --no-cpu-baseline > $out/drv200_$tag.log 2>&1 \
+    || fail drv200 $out/drv200_$tag.log
+  tail -1 $out/drv200_$tag.log | cut -c1-400
+fi
 if has kt; then
   cd /tmp
   # the bench's timed frames (no moving camera: the in-flight instance's last 50 launches are the timed
@@ -117,6 +135,23 @@ print(json.dumps({'variant': '$v', 'bands': $n, 'streams': $s, 'round': $r, 'ms_
     done
   done
   cat $out/sbab_$tag.jsonl
+fi
+if has lines; then
+  # bench lines alternated over LINES_ROUNDS rounds: LINES="args a|args b|..." (each a bench.py argument set,
+  # --no-cpu-baseline --moving-frames 0 added); one summary JSON line per run into lines_<tag>.jsonl
+  IFS='|' read -ra sets <<< "${LINES:?LINES}"
+  for r in $(seq ${LINES_ROUNDS:-2}); do
+    for i in "${!sets[@]}"; do
+      a="${sets[$i]}"
+      f=$out/lines_${tag}_${i}_$r.log
+      timeout -k 10 300 python bench.py --no-cpu-baseline --moving-frames 0 $a > $f 2>&1 || fail lines-$i $f
+      grep '^{' $f | tail -1 | LARGS="$a" R=$r python3 -c "import sys, json, os; d = json.loads(sys.stdin.read()); \
+c = d['config']; print(json.dumps({'args': os.environ['LARGS'], 'round': int(os.environ['R']), 'mrays': round(d['value'], 1), \
+'ms_per_step': round(d['ms_per_step'], 5), 'kernel_ms': round(c['kernel_ms_per_frame'], 5), \
+'lone_kernel_ms': round(c['lone_kernel_ms_per_frame'], 5), 'launch': c.get('timed_launch')}))" >> $out/lines_$tag.jsonl
+    done
+  done
+  cat $out/lines_$tag.jsonl | cut -c1-300
 fi
 if has cfg; then
   for c in C2 C4 C5; do

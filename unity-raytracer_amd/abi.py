@@ -13,7 +13,10 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "librt_mi355.so")
 
-RT_ABI_VERSION = 5
+RT_ABI_VERSION = 6
+# earlier ABIs an A/B variant may have: version 5 lacks rt_render_device_batch only
+OLDER_ABI_OK = (5,)
+RT_MAX_BATCH = 8
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -225,6 +228,8 @@ SIGNATURES = {
                             C.POINTER(rt_render_params), _P, C.POINTER(rt_stats)]),
     "rt_render_device": (C.c_int, [_P, C.POINTER(rt_camera), C.POINTER(rt_image_plane),
                                    C.POINTER(rt_render_params), _P, C.c_size_t, C.POINTER(rt_stats)]),
+    "rt_render_device_batch": (C.c_int, [_P, C.c_int32, _P, C.POINTER(rt_image_plane),
+                                         C.POINTER(rt_render_params), _P, C.c_size_t, C.POINTER(rt_stats)]),
     "rt_band_rows_local": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32, C.c_int32]),
     "rt_assemble_bands": (C.c_int, [_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P]),
     "rt_pixel_bytes": (C.c_int32, [C.c_int32]),
@@ -258,13 +263,16 @@ def load_library(path: str | None = None):
             f"rt_mi355 HIP library not found at {p}; build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
     lib = C.CDLL(p)
+    # an explicitly named older build (a tools/abx.py or bench.py --lib A/B
+    # variant) may lack later entry points: those stay unbound (AttributeError if used)
+    older = path is not None and lib.rt_abi_version() in OLDER_ABI_OK
     for name, (res, args) in SIGNATURES.items():
-        if path is not None and name.startswith("rt_debug") and not hasattr(lib, name):
-            continue  # an older measuring build (tools/abx.py variants) without a later testing entry point
+        if (older or (path is not None and name.startswith("rt_debug"))) and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rt_abi_version() != RT_ABI_VERSION:
+    if lib.rt_abi_version() != RT_ABI_VERSION and not older:
         raise RuntimeError(f"rt_mi355 ABI mismatch: library {lib.rt_abi_version()} != {RT_ABI_VERSION}")
     if path is None:
         _lib = lib

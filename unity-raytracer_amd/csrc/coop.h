@@ -37,7 +37,8 @@ using rtm::f3;
 using rtm::mk;
 
 constexpr int kPopMax = 16;  // entries tested per iteration (4 lanes each)
-static_assert(rtd::kMaxBounces * 6 <= rtd::kStackTotal + rtd::kCutMax, "the fold of a one-sample wave fits its packet stack (trace.hip)");
+// (the fold buffer shade_wave writes is the wave's packet stack: asserted
+// against rtp::kWaveStack next to shade_wave in trace.hip)
 
 // Push the lanes' `push` entries (ref, key) onto the wave's LDS stack at sp.
 // SORT (closest hit): nearest on top — an entry's position is the number of

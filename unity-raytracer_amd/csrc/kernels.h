@@ -59,6 +59,12 @@ hipError_t launch_refresh_cut(const rtd::BvhNode4 *nodes, rtd::CutTable *out, hi
 hipError_t launch_render_mega(const rtd::SceneDev &S, const rtd::FrameDev &F, bool count_tests,
                               hipStream_t stream, const char **instance = nullptr);
 
+// The frames of a batch (rtd::FrameBatch: whole 4-spp frames of one layout)
+// in one launch: render_batch_kernel, then the batch's sky tail and tallies
+// (sky_batch_batch_kernel) or its tallies alone.
+hipError_t launch_render_batch(const rtd::SceneDev &S, const rtd::FrameBatch &B, hipStream_t stream,
+                               const char **instance = nullptr);
+
 // Level-synchronous all-packet megakernel (trace_levels.hip), chosen by
 // launch_render_mega for >= 16 spp on a 4-wide BVH.
 hipError_t launch_render_levels(const rtd::SceneDev &S, const rtd::FrameDev &F, hipStream_t stream);

@@ -30,20 +30,26 @@ int rt_create(rt_ctx **out_ctx, int32_t num_gpus) {
     if (num_gpus == 1) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return fail(nullptr, RT_E_NO_DEVICE, "hipGetDevice failed");
-        return create_one(dev, out_ctx);
+        const int st = create_one(dev, out_ctx);
+        if (st == RT_OK) register_ctx(*out_ctx);
+        return st;
     }
     if (num_gpus > count)
         return fail(nullptr, RT_E_NO_DEVICE, "num_gpus %d > %d visible devices", num_gpus, count);
     std::vector<int32_t> devs((size_t)num_gpus);
     for (int i = 0; i < num_gpus; ++i) devs[(size_t)i] = i;
-    return create_group(devs.data(), num_gpus, 0, out_ctx);
+    const int st = create_group(devs.data(), num_gpus, 0, out_ctx);
+    if (st == RT_OK) register_ctx(*out_ctx);
+    return st;
 }
 
 int rt_create_devices(rt_ctx **out_ctx, const int32_t *devices, int32_t num_devices, int32_t gather) {
     if (!out_ctx) return fail(nullptr, RT_E_INVALID, "out_ctx is null");
     *out_ctx = nullptr;
     if (num_devices < 1 || !devices) return fail(nullptr, RT_E_INVALID, "need at least one device");
-    return create_group(devices, num_devices, gather, out_ctx);
+    const int st = create_group(devices, num_devices, gather, out_ctx);
+    if (st == RT_OK) register_ctx(*out_ctx);
+    return st;
 }
 
 int rt_get_device_info(const rt_ctx *ctx, rt_device_info *info) {
@@ -59,7 +65,8 @@ int rt_get_device_info(const rt_ctx *ctx, rt_device_info *info) {
 void rt_destroy(rt_ctx *ctx) {
     if (!ctx) return;
     DeviceGuard guard;
-    ctx->destroying.store(true);  // host_waits_report no longer reads the context
+    unregister_ctx(ctx);  // waits for a report reading it; later reports do not read it
+    ctx->destroying.store(true);
     release_group(ctx);
     destroy_one(ctx);
 }
@@ -244,6 +251,60 @@ int rt_render_device(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane 
         return fail(ctx, RT_E_INVALID, "output buffer %zu bytes < %zu required", out_bytes, bytes);
     HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
     return run_frame(ctx, F, params, d_out_rgba, stats, t0, nullptr, 0);
+}
+
+int rt_render_device_batch(rt_ctx *ctx, int32_t num_frames, const rt_camera *cameras, const rt_image_plane *plane,
+                           const rt_render_params *params, void *d_out, size_t frame_stride_bytes, rt_stats *stats) {
+    if (!ctx) return RT_E_INVALID;
+    auto t0 = std::chrono::steady_clock::now();
+    DeviceGuard guard;
+    if (num_frames < 1 || num_frames > RT_MAX_BATCH)
+        return fail(ctx, RT_E_INVALID, "num_frames %d outside [1, %d]", num_frames, RT_MAX_BATCH);
+    if (!cameras || !plane || !params) return fail(ctx, RT_E_INVALID, "null cameras/plane/params");
+    static_assert(RT_MAX_BATCH == rtd::kMaxBatch, "rt_mi355.h RT_MAX_BATCH");
+    const bool group = !ctx->peers.empty() || ctx->gather == RT_GATHER_RCCL;
+    rtd::FrameDev F[RT_MAX_BATCH];
+    size_t bytes = 0;
+    bool one_launch = !group;
+    if (one_launch) {
+        for (int i = 0; i < num_frames; ++i) {
+            const int st = prepare_frame(ctx, &cameras[i], plane, params, F[i], bytes);
+            if (st) return st;
+        }
+        one_launch = batch_launchable(ctx, F[0], params, num_frames);
+    }
+    if (!one_launch) {
+        // frames one by one (the same frames; stats summed, device time added)
+        rt_stats sum{}, one{};
+        for (int i = 0; i < num_frames; ++i) {
+            const int st = rt_render_device(ctx, &cameras[i], plane, params, (char *)d_out + (size_t)i * frame_stride_bytes,
+                                            frame_stride_bytes, stats ? &one : nullptr);
+            if (st) return st;
+            if (!stats) continue;
+            sum.primary_rays += one.primary_rays;
+            sum.shadow_rays += one.shadow_rays;
+            sum.reflection_rays += one.reflection_rays;
+            sum.box_tests += one.box_tests;
+            sum.triangle_tests += one.triangle_tests;
+            sum.sphere_tests += one.sphere_tests;
+            sum.shading_fetches += one.shading_fetches;
+            sum.primary_scene_misses += one.primary_scene_misses;
+            sum.shadow_rays_moot += one.shadow_rays_moot;
+            sum.kernel_ms += one.kernel_ms;
+        }
+        if (stats) {
+            sum.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            *stats = sum;
+        }
+        return RT_OK;
+    }
+    if (bytes && !d_out) return fail(ctx, RT_E_INVALID, "d_out is null");
+    if (frame_stride_bytes < bytes)
+        return fail(ctx, RT_E_INVALID, "frame stride %zu bytes < %zu required", frame_stride_bytes, bytes);
+    HIP_OR_FAIL(ctx, hipSetDevice(ctx->device));
+    const BatchIn bi{F, num_frames, frame_stride_bytes};
+    rtd::FrameDev H = F[0];
+    return run_frame(ctx, H, params, d_out, stats, t0, nullptr, 0, &bi);
 }
 
 int rt_assemble_bands(rt_ctx *ctx, const float *d_gathered, int32_t resolution_x, int32_t resolution_y,

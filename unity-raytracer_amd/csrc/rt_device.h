@@ -282,4 +282,19 @@ struct FrameDev {
     int *persist_ctr;
 };
 
+// The frames of one batch launch (trace.hip render_batch_kernel,
+// rt_render_device_batch): frames of one layout from their own cameras, whose
+// tiles form one index space — batch tile f * frame_tiles + t is tile t of
+// frame f.  Every f[i] carries the batch's dispatch fields (num_tiles = frames
+// x frame_tiles, tile_order / tile_cost over batch tiles, splits, sky tail,
+// tallies, counters); its camera-derived constants and output are its own.
+// Passed by value (kernel arguments, scalar loads): kMaxBatch x 408 B.
+constexpr int kMaxBatch = 8;
+struct FrameBatch {
+    FrameDev f[kMaxBatch];
+    int frames;                  // 1 .. kMaxBatch
+    int frame_tiles;             // tiles of one frame
+    unsigned frame_tiles_magic;  // floor(2^32 / frame_tiles) (0xffffffff for 1)
+};
+
 }  // namespace rtd

@@ -457,6 +457,9 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // (a counting launch measures tests, not costs: its per-lane walk is not the
     // frame a longest-first order is for, and it never answers a tile as sky)
     if (!mega || count || (prm->flags & RT_FLAG_ROW_ORDER) != 0 || F.num_tiles <= 0) return RT_OK;
+    // a batch launch (rt_render_device_batch): its 6-wave instances split tiles
+    // into quarter- and one-pixel waves, never one-sample waves
+    const bool batch = slab >= kBatchSlab;
     for (LptSlot &l : ctx->lpt)
         if (l.used && l.stream == ctx->stream && l.slab == slab) ls = &l;
     if (!ls)
@@ -516,7 +519,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         // sixteenth-waves (4 lanes) must hold whole pixels too
         if (kSplit16Div > 0 && 4 % F.spp == 0) {
             // a lone shard's (one-sample waves, below) more (kSplit16DivSample)
-            const bool sample_waves = F.spp == 4 && !overlapped_frame(ctx, prm) && group_sample_waves(ctx);
+            const bool sample_waves = F.spp == 4 && !overlapped_frame(ctx, prm) && group_sample_waves(ctx) && !batch;
             const int div = sample_waves ? kSplit16DivSample : kSplit16Div;
             F.split16_tiles = std::min(F.split_tiles, std::max(1, F.num_tiles / div));
             F.split_tiles -= F.split16_tiles;
@@ -525,7 +528,8 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
                (F.num_tiles <= kSplit16MaxTiles || (kSplitSync && !overlapped_frame(ctx, prm)))) {
         const bool lone_shard = F.num_tiles <= kSplit16MaxTiles && !overlapped_frame(ctx, prm);
         // (one-sample waves below: kSplit16DivLoneSample)
-        const bool sample_waves = lone_shard && F.spp == 4 && F.num_tiles <= kSample16LoneTiles && group_sample_waves(ctx);
+        const bool sample_waves =
+            lone_shard && F.spp == 4 && F.num_tiles <= kSample16LoneTiles && group_sample_waves(ctx) && !batch;
         const int div = sample_waves ? kSplit16DivLoneSample
                         : lone_shard ? kSplit16DivLone
                         : F.num_tiles > kSplit16MaxTiles ? kSplit16DivWhole : kSplit16DivLarge;
@@ -557,7 +561,7 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     // frame too, unless rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0)
     // (group_sample_waves above).
     if (F.split16_tiles > 0 && !count && !levels && F.spp == 4 && F.num_tiles <= rtk::kShardTilesMax &&
-        F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm) && group_sample_waves(ctx)) {
+        F.num_tiles <= kSample16LoneTiles && !overlapped_frame(ctx, prm) && group_sample_waves(ctx) && !batch) {
         F.s16_shift = 0;
         const size_t sb = (size_t)F.split16_tiles * rtd::kWaveSize * 4 * sizeof(float);
         const size_t cb = (size_t)F.split16_tiles * (rtd::kWaveSize / 4) * sizeof(int);
@@ -581,9 +585,10 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         // (render_kernel keeps one wave at least: its launch and tallies stay, an all-sky view included)
         F.sky_batch_tiles = std::max(0, std::min(ls->sky_tail, F.num_tiles - F.split_tiles - F.split16_tiles - 1));
     {
-        char b[128];
-        snprintf(b, sizeof b, " lpt: frame=%lld sky_tail=%d known=%d pending=%d overlapped=%d", ls->frames,
-                 ls->sky_tail, (int)ls->sky_known, (int)ls->sky_pending, (int)overlapped_frame(ctx, prm));
+        char b[160];
+        snprintf(b, sizeof b, " lpt: frame=%lld sky_tail=%d known=%d pending=%d overlapped=%d sky_waits=%lld",
+                 ls->frames, ls->sky_tail, (int)ls->sky_known, (int)ls->sky_pending, (int)overlapped_frame(ctx, prm),
+                 ctx->sky_waits);
         ctx->last_lpt = b;
     }
     if (levels && !(F.max_bounces > rtd::kMaxBounces)) {
@@ -638,6 +643,17 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
     return RT_OK;
 }
 
+// Whether a frame like F (same layout, same overlap) takes sky batches, i.e.
+// whether the sky tail of F's order is worth a host wait (lpt_prepare's rules:
+// megakernel frames in flight of more than kSkyMinTiles tiles, 16-spp levels
+// frames in flight).  Lone frames, small shares and rt_render's row slabs
+// never use the tail, so their first sort does not wait for its count.
+static bool sky_tail_usable(const rt_ctx *ctx, const rtd::FrameDev &F) {
+    if (rtk::kSkyBatch <= 1 || F.max_bounces > rtd::kMaxBounces) return false;
+    if (ctx->S.bvh4 && F.spp >= 16) return F.spp == 16 && F.in_flight;
+    return F.num_tiles > kSkyMinTiles && (F.in_flight || (kSkyLone && F.num_tiles > rtk::kShardTilesMax));
+}
+
 int lpt_sort_now(rt_ctx *ctx, const rtd::FrameDev &F, LptSlot *ls) {
     HIP_OR_FAIL(ctx, rtk::sort_tiles_by_cost((const unsigned *)ls->cost.p, (unsigned *)ls->cost_sorted.p,
                                              (const int *)ls->iota.p, (int *)ls->order.p, F.num_tiles,
@@ -651,10 +667,13 @@ int lpt_sort_now(rt_ctx *ctx, const rtd::FrameDev &F, LptSlot *ls) {
         HIP_OR_FAIL(ctx, rtk::launch_sky_count((const unsigned *)ls->cost_sorted.p, F.num_tiles, ++ls->sky_seq, dev,
                                                ctx->stream));
         ls->sky_pending = true;
-        if (!ls->sky_known) {
-            // the slot's first order: wait for its count once (frames in
-            // flight run far ahead of the device, so a lagged count of the
-            // first sort would arrive only after the frames that need it)
+        if (!ls->sky_known && sky_tail_usable(ctx, F)) {
+            // the slot's first order that a frame in flight can use: wait for
+            // its count once (frames in flight run far ahead of the device, so
+            // a lagged count of the first sort would arrive only after the
+            // frames that need it); other frames read it later, untagged
+            // counts are never used (lpt_prepare)
+            ++ctx->sky_waits;
             if (!ls->sky_ev) HIP_OR_FAIL(ctx, hipEventCreateWithFlags(&ls->sky_ev, hipEventDisableTiming));
             HIP_OR_FAIL(ctx, hipEventRecord(ls->sky_ev, ctx->stream));
             HIP_WAIT(ctx, hipEventSynchronize(ls->sky_ev));
@@ -686,8 +705,56 @@ Path frame_path(const rt_ctx *ctx, const rt_render_params *prm) {
     return p;
 }
 
-// Enqueues the trace launch(es) of F on the context's stream.
-int launch_frame(rt_ctx *ctx, rtd::FrameDev &F, const Path &P, const rtw::Args &A, int chunk_tiles) {
+// The frames of a batch launch (batch_frame: whole frames of one layout, one
+// launch; F is its head).  The dispatch fields lpt_prepare set on the head
+// are the batch's: every frame block carries them, with its own camera
+// constants and output.
+static void fill_batch(const rtd::FrameDev &H, const BatchIn &bi, rtd::FrameBatch &B) {
+    std::memset(&B, 0, sizeof B);
+    B.frames = bi.n;
+    B.frame_tiles = bi.frames[0].num_tiles;
+    B.frame_tiles_magic = B.frame_tiles <= 1 ? 0xffffffffu : (unsigned)((1ull << 32) / (unsigned long long)B.frame_tiles);
+    for (int i = 0; i < bi.n; ++i) {
+        rtd::FrameDev &f = B.f[i];
+        f = bi.frames[i];
+        f.out = (char *)H.out + (size_t)i * bi.stride;
+        f.counters = H.counters;
+        f.num_tiles = H.num_tiles;
+        f.tile_order = H.tile_order;
+        f.tile_cost = H.tile_cost;
+        f.split16_tiles = H.split16_tiles;
+        f.split_tiles = H.split_tiles;
+        f.sky_batch_tiles = H.sky_batch_tiles;
+        f.s16_shift = H.s16_shift;
+        f.split_samples = H.split_samples;
+        f.split_count = H.split_count;
+        f.shadow_hint = nullptr;  // (the batch instances take no occluder hints)
+        f.wave_counts = H.wave_counts;
+        f.count_tag = H.count_tag;
+        f.in_flight = H.in_flight;
+        f.wave_clock = H.wave_clock;
+    }
+}
+
+// Enqueues the trace launch(es) of F on the context's stream (bi: F is the
+// head of a batch launch).
+int launch_frame(rt_ctx *ctx, rtd::FrameDev &F, const Path &P, const rtw::Args &A, int chunk_tiles,
+                 const BatchIn *bi) {
+    if (bi) {
+        static thread_local rtd::FrameBatch B;  // (3.3 KB: off the stack)
+        fill_batch(F, *bi, B);
+        const char *inst = nullptr;
+        HIP_OR_FAIL(ctx, rtk::launch_render_batch(ctx->S, B, ctx->stream, &inst));
+        if (inst) {
+            char b[256];
+            snprintf(b, sizeof b, "%s frames=%d tiles=%d split16=%d split=%d s16_shift=%d rows=%d band=%d/%d sky=%d",
+                     inst, bi->n, F.num_tiles, F.split16_tiles, F.split_tiles, F.s16_shift, F.local_rows, F.band_index,
+                     F.band_count, F.sky_batch_tiles);
+            ctx->last_launch = b;
+            ctx->last_launch += ctx->last_lpt;
+        }
+        return RT_OK;
+    }
     if (P.packet)
         HIP_OR_FAIL(ctx, rtk::launch_render_packet(ctx->S, F, P.count, ctx->stream));
     else if (P.mega) {
@@ -707,11 +774,22 @@ int launch_frame(rt_ctx *ctx, rtd::FrameDev &F, const Path &P, const rtw::Args &
     return RT_OK;
 }
 
+bool batch_launchable(const rt_ctx *ctx, const rtd::FrameDev &F, const rt_render_params *prm, int n) {
+    const Path P = frame_path(ctx, prm);
+    return n > 1 && n <= rtd::kMaxBatch && P.mega && !P.count && F.spp == 4 && F.tile_w == 4 && F.tile_h == 4 &&
+           F.max_bounces <= rtd::kMaxBounces && F.num_tiles > 0 && (long long)F.num_tiles * n < (1ll << 30);
+}
+
 int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *d_out, rt_stats *stats,
-              std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes) {
-    Range range("rt_frame");
+              std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes, const BatchIn *bi) {
+    Range range(bi ? "rt_frame_batch" : "rt_frame");
     F.out = d_out;
     F.counters = ctx->d_counters;
+    if (bi) {
+        // the batch's head: its tiles are every frame's (one index space)
+        if (host_out) return fail(ctx, RT_E_INVALID, "a batch renders into device memory");
+        F.num_tiles = bi->frames[0].num_tiles * bi->n;
+    }
     const Path P = frame_path(ctx, prm);
     const bool async = (prm->flags & RT_FLAG_ASYNC) != 0;
     if (async && host_out) return fail(ctx, RT_E_INVALID, "RT_FLAG_ASYNC needs a device output (rt_render_device)");
@@ -798,7 +876,8 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         Launch L{};
         L.F = F;
         L.stream = base;
-        int st = lpt_prepare(ctx, L.F, prm, P.mega, P.count, 0, L.ls, L.sort);
+        // (a batch keeps its order apart from single frames on the same stream: slot kBatchSlab + frames)
+        int st = lpt_prepare(ctx, L.F, prm, P.mega, P.count, bi ? kBatchSlab + bi->n : 0, L.ls, L.sort);
         if (st) return st;
         launches.push_back(L);
     }
@@ -831,7 +910,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             ctx->stream = launches[k].stream;
             if (k == ctx->debug_fail_slab)  // rt_debug_set(RT_DEBUG_FAIL_SLAB): tests only
                 return fail(ctx, RT_E_INTERNAL, "injected failure before slab %d (RT_DEBUG_FAIL_SLAB)", k);
-            int st = launch_frame(ctx, launches[k].F, P, A, chunk_tiles);
+            int st = launch_frame(ctx, launches[k].F, P, A, chunk_tiles, nullptr);
             if (st) return st;
             HIP_OR_FAIL(ctx, hipEventRecord(ctx->slab_done[k], ctx->stream));
             // the copier thread copies slab k once its launch has ended, while
@@ -859,7 +938,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         HIP_OR_FAIL(ctx, ctx->copier.wait());  // every slab is in the caller's buffer
     } else {
         Launch &L = launches[0];
-        int st = launch_frame(ctx, L.F, P, A, chunk_tiles);
+        int st = launch_frame(ctx, L.F, P, A, chunk_tiles, bi);
         if (st) return st;
         if (async) {
             if (L.sort) {

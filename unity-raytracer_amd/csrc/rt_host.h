@@ -209,6 +209,10 @@ class Wait {
     long long prev_since_;
 };
 std::string host_waits_report(rt_ctx *ctx);
+// The registry of live contexts host_waits_report may read (rt_create* register
+// a context, rt_destroy unregisters it before tearing it down).
+void register_ctx(const rt_ctx *ctx);
+void unregister_ctx(const rt_ctx *ctx);
 
 // rt_render's host-output copies, issued from a thread of their own: a copy
 // into pageable memory holds the calling thread until it is done, so the
@@ -383,7 +387,8 @@ struct rt_ctx {
     bool debug_group_sample_waves = true;  // rt_debug_set(RT_DEBUG_GROUP_SAMPLE_WAVES, 0): group bands without them
     std::atomic<bool> destroying{false};  // rt_destroy has begun (host_waits_report skips the context)
     std::string last_launch;
-    std::string last_lpt;  // the longest-first slot's state of the last launch (RT_DEBUG_LAST_LAUNCH)  // the last render launch's kernel instance and split shape (RT_DEBUG_LAST_LAUNCH)
+    std::string last_lpt;  // the longest-first slot's state of the last launch (RT_DEBUG_LAST_LAUNCH)
+    long long sky_waits = 0;  // host waits for a first sort's sky-tail count (lpt_sort_now; RT_DEBUG_LAST_LAUNCH)
     rti::GrowBuf wave_clock;
     int64_t wave_clock_bytes = 0;
 };
@@ -436,8 +441,21 @@ int update_mesh_transforms_one(rt_ctx *ctx, const float *local_to_world, int32_t
 // ---- frames (rt_frame.cpp)
 int prepare_frame(rt_ctx *ctx, const rt_camera *cam, const rt_image_plane *plane, const rt_render_params *prm,
                   rtd::FrameDev &F, size_t &out_bytes);
+// The frames of a batch launch (rt_render_device_batch): n frames of one
+// layout, prepared from their cameras, outputs `stride` bytes apart.
+struct BatchIn {
+    const rtd::FrameDev *frames;
+    int n;
+    size_t stride;
+};
+// longest-first slots of batches: slab kBatchSlab + frames (apart from single frames)
+constexpr int kBatchSlab = 1000;
+// Whether n frames like F can go as one batch launch (4 spp megakernel frames).
+bool batch_launchable(const rt_ctx *ctx, const rtd::FrameDev &F, const rt_render_params *prm, int n);
+// bi: F is the head of a batch (prepared like its first frame), rendered as one launch
 int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *d_out, rt_stats *stats,
-              std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes);
+              std::chrono::steady_clock::time_point t_start, void *host_out, size_t out_bytes,
+              const BatchIn *bi = nullptr);
 void free_wavefront(rt_ctx *c);
 int settle_async(rt_ctx *ctx);
 void fill_stats(rt_stats *stats, const unsigned long long counts[rtd::kCounterWords], double kernel_ms,

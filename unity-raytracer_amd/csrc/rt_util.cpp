@@ -3,6 +3,7 @@
 #include "rt_host.h"
 
 #include <atomic>
+#include <unordered_set>
 
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -84,6 +85,26 @@ void stream_line(std::string &o, const char *who, int member, int dev, hipStream
 }
 }  // namespace
 
+// ---- live contexts: the report reads a context only while it is registered,
+// under the registry's lock, and rt_destroy unregisters it (taking the same
+// lock) before any teardown — so a report from another thread never reads a
+// context being destroyed or freed (it only compares the pointer value).
+namespace {
+std::mutex g_live_mu;
+std::unordered_set<const rt_ctx *> g_live;
+}  // namespace
+
+void register_ctx(const rt_ctx *ctx) {
+    if (!ctx) return;
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.insert(ctx);
+}
+
+void unregister_ctx(const rt_ctx *ctx) {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.erase(ctx);
+}
+
 std::string host_waits_report(rt_ctx *ctx) {
     std::string o = "host threads inside blocking library calls:\n";
     const long long t = now_ns();
@@ -100,7 +121,9 @@ std::string host_waits_report(rt_ctx *ctx) {
     }
     if (!n) o += "  (none)\n";
     if (!ctx) return o;
-    if (ctx->destroying.load()) return o + "context: being destroyed (rt_destroy), not read\n";
+    std::lock_guard<std::mutex> live(g_live_mu);  // held while the context is read
+    if (!g_live.count(ctx) || ctx->destroying.load())
+        return o + "context: not live (destroyed or being destroyed by rt_destroy), not read\n";
     DeviceGuard guard;
     o += "streams of the context:\n";
     for (int m = 0; m < nmembers(ctx); ++m) {

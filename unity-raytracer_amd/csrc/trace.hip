@@ -12,6 +12,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 
 #include <hip/hip_runtime.h>
@@ -466,6 +467,8 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
 // traversal.  The mirror fold (c + km*(...), back to front) sits in the
 // wave's LDS: `fold` holds 6 floats per level (kMaxBounces levels).  Tallies
 // are wave-uniform.
+// (the fold sits in the wave's packet-stack LDS, wstack: rtp::kWaveStack ints)
+static_assert(kMaxBounces * 6 <= rtp::kWaveStack, "a one-sample wave's mirror fold fits its packet stack");
 __device__ __forceinline__ f3 shade_wave(const SceneDev &S, const FrameDev &F, f3 o, f3 d, int2 *stk, int wide,
                                          float *fold, unsigned &n_sh, unsigned &n_rf, unsigned &n_mo) {
     int depth = 0;
@@ -609,6 +612,19 @@ constexpr bool kCoopSampleWaves = false;
 constexpr bool kCoopSampleWaves = true;
 #endif
 
+// The frame of batch tile t (t = f * frame_tiles + tile, wave-uniform) by the
+// batch's magic multiplier (no integer division), and its tile in the frame.
+__device__ __forceinline__ const FrameDev &batch_frame(const FrameBatch &B, int t, int &tile) {
+    unsigned q = __umulhi((unsigned)t, B.frame_tiles_magic);
+    int r = t - (int)q * B.frame_tiles;
+    if (r >= B.frame_tiles) {
+        ++q;
+        r -= B.frame_tiles;
+    }
+    tile = r;
+    return B.f[q];
+}
+
 // SPLIT: the variant launched when a frame splits tiles (a separate instance, so
 // the common kernel's code and register allocation stay as they are); DEEP:
 // the one for MaxReflectionBounces > kMaxBounces (deep_chain); Q4: frames of
@@ -618,9 +634,15 @@ constexpr bool kCoopSampleWaves = true;
 // own instance, so the shard instance that frames in flight run keeps its
 // register allocation (the whole-wave path beside it: +11 VGPR and +65 SGPR
 // spill slots, in-flight 1/2 and 1/4 shares 9-14 % slower, r05n).
-template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false, int W = kMkMinWaves,
-          bool SAMPLE = false>
-__global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, FrameDev F) {
+//
+// BATCH (render_batch_kernel): the frames of a FrameBatch in one launch — the
+// batch's tiles are one index space (frame f's tile t is f * frame_tiles + t),
+// dispatched and measured by one longest-first order; each wave renders its
+// tile with its own frame's constants (camera, sky and frustum constants,
+// output), the dispatch fields (order, splits, tallies) are the batch's and
+// equal in every frame's block.
+template <bool COUNT, bool SPLIT, bool DEEP, bool Q4, int W, bool SAMPLE, bool BATCH>
+__device__ __forceinline__ void render_wave(const SceneDev &S, const FrameDev &F, const FrameBatch *B) {
     // the per-lane LDS stack: kStackSize entries where six waves per SIMD must
     // fit the CU's LDS, kStackShard at five (fewer overflows to scratch)
     constexpr int SS = W >= 6 ? kStackSize : kStackShard;
@@ -703,6 +725,9 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     int tile = idx;
     if (F.tile_order) tile = rtt::cload(F.tile_order + idx);
     tile = __builtin_amdgcn_readfirstlane(tile);
+    // a batch: the frame of the batch tile and its tile within the frame
+    int ftile = tile;
+    const FrameDev &FF = BATCH ? batch_frame(*B, tile, ftile) : F;
     // the launch's camera samples (one per active lane of every tile, computed
     // by the host: rt_device.h active_samples), counted once per launch
     if (!COUNT && !F.wave_counts && wid == 0 && lane == 0) atomicAdd(rtt::counter_slot(F.counters), F.primary_total);
@@ -717,9 +742,9 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
     // wave on the sample's ray chain (wave-uniform test)
     if (SAMPLE && kCoopSampleWaves && HINT && !COUNT && !DEEP && pshift == 0 && (Q4 || F.spp == 4) && S.bvh4 &&
         F.max_bounces <= kMaxBounces)
-        sky = render_sample_wave<Q4>(S, F, st, wstack, tile, part, idx, cnt);
+        sky = render_sample_wave<Q4>(S, FF, st, wstack, ftile, part, idx, cnt);
     else
-        sky = render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, F, st, wstack, tile, part, pshift, lane, cnt, sg, idx);
+        sky = render_tile<COUNT, DEEP, Q4, HINT, SPLIT>(S, FF, st, wstack, ftile, part, pshift, lane, cnt, sg, idx);
     const int lane_e = rtt::lane_id();  // not kept live across the trace
     if (F.tile_cost && lane_e == 0 && part <= 0) {
         // a sky tile's key is 0: the next frames dispatch the sky tiles last, in row order
@@ -772,6 +797,21 @@ __global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, Frame
 #endif
 }
 
+template <bool COUNT, bool SPLIT = false, bool DEEP = false, bool Q4 = false, int W = kMkMinWaves,
+          bool SAMPLE = false>
+__global__ __launch_bounds__(kMkThreads, W) void render_kernel(SceneDev S, FrameDev F) {
+    render_wave<COUNT, SPLIT, DEEP, Q4, W, SAMPLE, false>(S, F, nullptr);
+}
+
+// The frames of a batch in one launch (rt_render_device_batch: frames in
+// flight of one layout, e.g. the frames of one gather group of a rank's row
+// band): whole frames' 6-wave instances, Q4 only; B.f[0] holds the batch's
+// dispatch fields.
+template <bool SPLIT>
+__global__ __launch_bounds__(kMkThreads, kMkMinWaves) void render_batch_kernel(SceneDev S, FrameBatch B) {
+    render_wave<false, SPLIT, false, true, kMkMinWaves, false, true>(S, B.f[0], &B);
+}
+
 // The sky tail of a longest-first order (the last F.sky_batch_tiles
 // positions: the tiles the last measurement found to be sky), rtk::kSkyBatch
 // tiles a wave, launched after render_kernel on its stream.  A sky tile is a
@@ -810,38 +850,113 @@ __device__ __forceinline__ void wave_counts_part(const FrameDev &F, int waves, i
     }
 }
 
+// A tile of a sky tail that is not sky this frame (the order predates a
+// camera or scene change): rendered in full, as render_kernel's whole-frame
+// instance would, after the sky loop (sky_batch_wave) — which keeps only its
+// loop state live, not the tile path's frame constants (with render_tile
+// inside the sky loop the kernel had 152 VGPR / 163 SGPR spill slots and wrote
+// 1.6x its sky pixels, round 5).  The tallies go to the counters directly.
+// pos: the tile's position in the order.
+// The sky kernels' one argument: its kernel-argument segment is this block,
+// which the out-of-line fallback reads through the segment pointer (scalar
+// loads; a callee's pointer arguments would arrive in VGPRs).
+template <bool BATCH>
+struct SkyArgs {
+    SceneDev S;
+    typename std::conditional<BATCH, FrameBatch, FrameDev>::type P;  // the frame, or the batch (P.f[0]: dispatch)
+    int sky_blocks, waves;
+};
+__device__ __forceinline__ const FrameDev &head(const FrameDev &F) { return F; }
+__device__ __forceinline__ const FrameDev &head(const FrameBatch &B) { return B.f[0]; }
+template <bool Q4, bool BATCH>
+__device__ __noinline__ void sky_fallback(int pos) {
+    constexpr int FX = Q4 ? 2 : 0;
+    // the kernel's argument block (SkyArgs: the segment's only argument), by
+    // the segment pointer: scalar loads, nothing passed in registers
+    typedef const __attribute__((address_space(4))) SkyArgs<BATCH> KArgs;
+    const SkyArgs<BATCH> &A = *(const SkyArgs<BATCH> *)(KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+    pos = __builtin_amdgcn_readfirstlane(pos);
+    const SceneDev &S = A.S;
+    const FrameDev &H = head(A.P);
+    __shared__ int stack_mem[kStackSize * kWaveSize];
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem, ovf, kStackSize};  // (+ lane per query: traverse)
+    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
+    const int tile = __builtin_amdgcn_readfirstlane(rtt::cload(H.tile_order + pos));
+    int ftile = tile;
+    const FrameDev &F = BATCH ? batch_frame(*(const FrameBatch *)&A.P, tile, ftile) : H;
+    const unsigned long long t0 = H.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
+    int px, ly, gy, s;
+    const bool active = rts::slot_pixel<FX>(F, ftile, rtt::lane_id(), px, ly, gy, s);
+    f3 color = mk(0.0f, 0.0f, 0.0f);
+    if (active) {
+        f3 o, d;
+        rts::primary_ray<FX>(F, px, gy, s, o, d);
+        // the per-lane Whitted loop (shade_levels, the mirror chains' path):
+        // the same answers as render_tile's packets, bit for bit
+        color = shade_levels<false, false, true>(S, F, o, d, 0, st, cnt);
+    }
+    const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
+    if (active && s == 0) {
+        f3 v = sum;
+        if (Q4)
+            v = v * 0.25f;
+        else if (F.spp > 1)
+            v = (F.spp & (F.spp - 1)) == 0 ? v * F.inv_spp : v / (float)F.spp;
+        rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+    }
+    if (H.tile_cost && rtt::lane_id() == 0)
+        H.tile_cost[tile] = max(1u, tile_cost_key(__builtin_amdgcn_s_memtime() - t0, -1, 4));
+    rtt::flush_counts<false>(cnt, H.counters);
+}
+
 // The work a frame in flight has after its render_kernel / levels launch, in
 // one launch on its stream (a second dependent launch per frame cost a 1/8
-// share in flight 35 %): blocks [0, sky_blocks) the order's sky tail, the
-// rest the launch's per-wave tallies (`waves` entries).
-template <bool Q4>
-__global__ __launch_bounds__(kMkThreads, kSkyWaves) void sky_batch_kernel(SceneDev S, FrameDev F, int sky_blocks,
-                                                                          int waves) {
+// share in flight 35 %): blocks [0, sky_blocks) the order's sky tail
+// (kSkyBatch tiles a wave: each a sky test and a background store,
+// sky_tile), the rest the launch's per-wave tallies (`waves` entries).  The
+// tiles that stopped being sky are noted in a wave-uniform mask during the
+// loop and rendered after it, out of line (sky_fallback).  BATCH: the tail of
+// a batch's order, each tile with its own frame's constants.
+// one-wave blocks: p0 is indexed by the block and wave_counts_part strides
+// the lanes with threadIdx & 63
+static_assert(kMkThreads == kWaveSize, "sky_batch_kernel runs one-wave blocks");
+static_assert(rtk::kSkyBatch <= 32, "the stale-tile mask");
+template <bool Q4, bool BATCH>
+__device__ __forceinline__ void sky_batch_wave(const SkyArgs<BATCH> &A) {
+    const FrameDev &H = head(A.P);
+    const int sky_blocks = A.sky_blocks, waves = A.waves;
     if ((int)blockIdx.x >= sky_blocks) {  // wave-uniform
-        wave_counts_part(F, waves, (int)blockIdx.x - sky_blocks, (int)gridDim.x - sky_blocks);
+        wave_counts_part(H, waves, (int)blockIdx.x - sky_blocks, (int)gridDim.x - sky_blocks);
         return;
     }
-    __shared__ int stack_mem[kStackSize * kWaveSize];
-    __shared__ int wstack_mem[rtp::kWaveStack];
-    int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem, ovf, kStackSize};
-    Counts cnt = {0, 0, 0, 0, 0, 0, 0};
-    const int p0 = F.num_tiles - F.sky_batch_tiles + (int)blockIdx.x * rtk::kSkyBatch;
-    const int n = min(rtk::kSkyBatch, F.num_tiles - p0);  // wave-uniform
+    const int p0 = H.num_tiles - H.sky_batch_tiles + (int)blockIdx.x * rtk::kSkyBatch;
+    const int n = min(rtk::kSkyBatch, H.num_tiles - p0);  // wave-uniform
+    unsigned stale = 0u;                                 // wave-uniform: bit j, position p0 + j is not sky
     for (int j = 0; j < n; ++j) {
-        const int tile = __builtin_amdgcn_readfirstlane(rtt::cload(F.tile_order + p0 + j));
-        if (sky_tile<Q4>(F, tile)) {
-            if (F.tile_cost && rtt::lane_id() == 0) F.tile_cost[tile] = 0u;  // still sky: dispatched last again
-            continue;
+        const int tile = __builtin_amdgcn_readfirstlane(rtt::cload(H.tile_order + p0 + j));
+        int ftile = tile;
+        const FrameDev &F = BATCH ? batch_frame(*(const FrameBatch *)&A.P, tile, ftile) : H;
+        if (sky_tile<Q4>(F, ftile)) {
+            if (H.tile_cost && rtt::lane_id() == 0) H.tile_cost[tile] = 0u;  // still sky: dispatched last again
+        } else {
+            stale |= 1u << j;
         }
-        const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
-        SegClock sg = {0ull, 0ull, 0ull, 0ull};
-        const bool sky = render_tile<false, false, Q4, false, false>(S, F, st, wstack_mem, tile, -1, 4,
-                                                                     threadIdx.x & 63, cnt, sg, p0 + j);
-        if (F.tile_cost && rtt::lane_id() == 0)
-            F.tile_cost[tile] = sky ? 0u : max(1u, tile_cost_key(__builtin_amdgcn_s_memtime() - t0, -1, 4));
     }
-    rtt::flush_counts<false>(cnt, F.counters);
+    while (stale) {  // (rare: a camera or scene change since the order's measurement)
+        const int j = __builtin_ctz(stale);
+        stale &= stale - 1u;
+        sky_fallback<Q4, BATCH>(p0 + j);
+    }
+}
+
+template <bool Q4>
+__global__ __launch_bounds__(kMkThreads, kSkyWaves) void sky_batch_kernel(SkyArgs<false> A) {
+    sky_batch_wave<Q4, false>(A);
+}
+
+__global__ __launch_bounds__(kMkThreads, kSkyWaves) void sky_batch_batch_kernel(SkyArgs<true> A) {
+    sky_batch_wave<true, true>(A);
 }
 
 // Per-wave tallies of a render_kernel launch (F.wave_counts) -> the frame's
@@ -1225,7 +1340,7 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         if (F.sky_batch_tiles > 0 && F.tile_order && F.wave_counts) {  // (16 spp in flight: the order's sky tail)
             const int sb = (F.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch;
             hipLaunchKernelGGL(sky_batch_kernel<false>, dim3(sb + tail_count_blocks(waves)), dim3(kMkThreads), 0, stream,
-                               S, F, sb, waves);
+                               SkyArgs<false>{S, F, sb, waves});
             return hipGetLastError();
         }
         if (!F.wave_counts) return hipGetLastError();
@@ -1244,15 +1359,47 @@ hipError_t launch_render_mega(const SceneDev &S, const FrameDev &F0, bool count_
         const int waves = render_mega_waves(F);
         const dim3 g(sb + tail_count_blocks(waves));
         if (q4)
-            hipLaunchKernelGGL(sky_batch_kernel<true>, g, dim3(kMkThreads), 0, stream, S, F, sb, waves);
+            hipLaunchKernelGGL(sky_batch_kernel<true>, g, dim3(kMkThreads), 0, stream, SkyArgs<false>{S, F, sb, waves});
         else
-            hipLaunchKernelGGL(sky_batch_kernel<false>, g, dim3(kMkThreads), 0, stream, S, F, sb, waves);
+            hipLaunchKernelGGL(sky_batch_kernel<false>, g, dim3(kMkThreads), 0, stream, SkyArgs<false>{S, F, sb, waves});
         return hipGetLastError();
     }
     if (!count_tests && F.wave_counts) {  // the launch's per-wave tallies -> counters
         const int waves = render_mega_waves(F);  // the entries lpt_prepare sized the buffer for
         hipLaunchKernelGGL(wave_counts_kernel, dim3(std::max(1, std::min(64, (waves + 1023) / 1024))), dim3(256), 0, stream,
                            (const uint4 *)F.wave_counts, waves, F.count_tag, F.primary_total, F.counters);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_render_batch(const SceneDev &S, const FrameBatch &B0, hipStream_t stream, const char **instance) {
+    const char *dummy = nullptr;
+    const char *&name = instance ? *instance : dummy;
+    name = nullptr;
+    if (B0.frames < 1 || B0.frames > kMaxBatch || B0.f[0].num_tiles <= 0) return hipErrorInvalidValue;
+    static thread_local FrameBatch B;
+    B = B0;
+    FrameDev &H = B.f[0];
+    // the batch's camera samples: one frame's times the frames
+    H.primary_total = active_samples(H.res_x, H.res_y, H.local_rows, H.row0, H.band_index, H.band_count,
+                                     H.band_rows, H.spp) *
+                      (unsigned long long)B.frames;
+    const int blocks = render_mega_waves(H);
+    if (H.split_tiles > 0 || H.split16_tiles > 0) {
+        hipLaunchKernelGGL(render_batch_kernel<true>, dim3(blocks), dim3(kMkThreads), 0, stream, S, B);
+        name = "render_batch_kernel<true>";
+    } else {
+        hipLaunchKernelGGL(render_batch_kernel<false>, dim3(blocks), dim3(kMkThreads), 0, stream, S, B);
+        name = "render_batch_kernel<false>";
+    }
+    if (H.sky_batch_tiles > 0 && H.tile_order && H.wave_counts) {
+        // the batch order's sky tail and the launch's tallies in one launch
+        const int sb = (H.sky_batch_tiles + rtk::kSkyBatch - 1) / rtk::kSkyBatch;
+        hipLaunchKernelGGL(sky_batch_batch_kernel, dim3(sb + tail_count_blocks(blocks)), dim3(kMkThreads), 0, stream,
+                           SkyArgs<true>{S, B, sb, blocks});
+    } else if (H.wave_counts) {
+        hipLaunchKernelGGL(wave_counts_kernel, dim3(std::max(1, std::min(64, (blocks + 1023) / 1024))), dim3(256), 0,
+                           stream, (const uint4 *)H.wave_counts, blocks, H.count_tag, H.primary_total, H.counters);
     }
     return hipGetLastError();
 }

@@ -210,6 +210,17 @@ class Context:
                                               C.c_void_p(dev_ptr), C.c_size_t(nbytes), C.byref(stats)))
         return stats
 
+    def render_device_batch(self, cameras, plane, params: abi.rt_render_params, dev_ptr: int, stride: int):
+        """rt_render_device_batch: len(cameras) frames of one layout as one
+        launch, frame i at dev_ptr + i * stride (device memory)."""
+        stats = abi.rt_stats()
+        cams = (abi.rt_camera * len(cameras))(
+            *[c if isinstance(c, abi.rt_camera) else camera_struct(c) for c in cameras])
+        pl = plane if isinstance(plane, abi.rt_image_plane) else plane_struct(plane)
+        self._check(self.lib.rt_render_device_batch(self.h, len(cameras), cams, C.byref(pl), C.byref(params),
+                                                    C.c_void_p(dev_ptr), C.c_size_t(stride), C.byref(stats)))
+        return stats
+
     def finish(self) -> abi.rt_stats:
         """Wait for RT_FLAG_ASYNC frames; their summed stats."""
         stats = abi.rt_stats()
