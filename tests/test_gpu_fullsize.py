@@ -19,6 +19,11 @@
 * C4 (3840x2160, 16 spp) and C5 (250k triangles, 64 spp, depth 16) whole
   frames (render_levels_kernel): every 16th row against the tree walk, plus
   brute force on seeded pixels.
+* C4's timed path (bench.py --config C4): four streams of RT_FLAG_ASYNC
+  frames, the levels kernel in flight with its 16-spp sky batches (the
+  measured non-sky tiles as stripes, the sky tail in sky_batch_kernel), every
+  16th row of every stream's frame against the tree walk, ray counts against
+  the counting launch, brute force on 64 seeded pixels.
 """
 import numpy as np
 import pytest
@@ -160,4 +165,54 @@ def test_levels_full_frame_every_16th_row(rt, orc, name):
     _same_bits(img[rows], ref, f"{name}: every 16th row vs the oracle's walk")
     assert st.primary_rays == W * H * fr.spp
     assert np.isfinite(img).all()
-    _brute_force(orc, fr, img, 64 if name == "C4" else 8, seed=13)
+    _brute_force(orc, fr, img, 64, seed=13)
+
+
+def test_c4_timed_path_in_flight_every_16th_row(rt, orc):
+    """bench.py --config C4's timed frames: the levels instance in flight with
+    its 16-spp sky batches (RT_DEBUG_LAST_LAUNCH sky > 0)."""
+    fr = rt.make("C4")
+    W, H = fr.plane.ResolutionX, fr.plane.ResolutionY
+    ctx = rt.Context()
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    try:
+        ctx.set_stream(streams[0].cuda_stream)
+        ctx.set_scene(fr.scene)
+        outs = [torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda") for _ in streams]
+        nbytes = outs[0].numel() * 4
+        # the counting launch (per-lane traversal, the canonical counts' path)
+        cst = ctx.render_device(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_COUNT_TESTS),
+                                outs[0].data_ptr(), nbytes)
+        p = rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC)
+        cam, pl = rt.raytracing.camera_struct(fr.camera), rt.raytracing.plane_struct(fr.plane)
+        for k, s in enumerate(streams):  # bench.py's setup: one untimed frame per stream
+            ctx.set_stream(s.cuda_stream)
+            ctx.render_device(cam, pl, p, outs[k].data_ptr(), nbytes)
+        ctx.finish()
+        torch.cuda.synchronize()
+        for o in outs:
+            o.fill_(float("nan"))
+        frames, launches = 8, []
+        for f in range(frames):
+            k = f % len(streams)
+            ctx.set_stream(streams[k].cuda_stream)
+            ctx.render_device(cam, pl, p, outs[k].data_ptr(), nbytes)
+            launches.append(ctx.last_launch())
+        st = ctx.finish()
+        torch.cuda.synchronize()
+        assert all(l.startswith("render_levels_kernel<6, 8, 4>") for l in launches), launches[:2]
+        sky = [int(l.split("sky=")[1].split()[0]) for l in launches[1:]]
+        assert all(s > 0 for s in sky), launches[:3]
+        rows = np.arange(0, H, 16)
+        imgs = [o[rows].cpu().numpy() for o in outs]
+        full0 = outs[0].cpu().numpy()
+        ctx.set_stream(None)
+        ref, _ = _walk(orc, fr, ctx, rows)
+    finally:
+        ctx.close()
+    for k in range(len(imgs)):
+        _same_bits(imgs[k], ref, f"C4 in flight, stream {k}: every 16th row vs the oracle's walk")
+    assert st.primary_rays == frames * W * H * fr.spp
+    assert tuple(getattr(st, k) for k in RAYS) == tuple(frames * getattr(cst, k) for k in RAYS)
+    assert np.isfinite(full0).all()
+    _brute_force(orc, fr, full0, 64, seed=14)

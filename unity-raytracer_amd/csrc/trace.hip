@@ -868,14 +868,16 @@ struct SkyArgs {
 };
 __device__ __forceinline__ const FrameDev &head(const FrameDev &F) { return F; }
 __device__ __forceinline__ const FrameDev &head(const FrameBatch &B) { return B.f[0]; }
+// (The argument block arrives as a pointer argument, i.e. in VGPRs, so the
+// loads of its fields here are vector loads: a rare path.  Not the kernarg
+// segment pointer builtin: a callee does not receive the segment pointer —
+// ROCm 7.2 compiles it from unrelated SGPRs, which faulted on the GPU.)
+template <bool BATCH>
+using KArgs = const __attribute__((address_space(4))) SkyArgs<BATCH> *;
 template <bool Q4, bool BATCH>
-__device__ __noinline__ void sky_fallback(int pos) {
+__device__ __noinline__ void sky_fallback(KArgs<BATCH> pa, int pos) {
     constexpr int FX = Q4 ? 2 : 0;
-    // the kernel's argument block (SkyArgs: the segment's only argument), by
-    // the segment pointer: scalar loads, nothing passed in registers
-    typedef const __attribute__((address_space(4))) SkyArgs<BATCH> KArgs;
-    const SkyArgs<BATCH> &A = *(const SkyArgs<BATCH> *)(KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
-    pos = __builtin_amdgcn_readfirstlane(pos);
+    const SkyArgs<BATCH> &A = *(const SkyArgs<BATCH> *)pa;
     const SceneDev &S = A.S;
     const FrameDev &H = head(A.P);
     __shared__ int stack_mem[kStackSize * kWaveSize];
@@ -946,7 +948,7 @@ __device__ __forceinline__ void sky_batch_wave(const SkyArgs<BATCH> &A) {
     while (stale) {  // (rare: a camera or scene change since the order's measurement)
         const int j = __builtin_ctz(stale);
         stale &= stale - 1u;
-        sky_fallback<Q4, BATCH>(p0 + j);
+        sky_fallback<Q4, BATCH>((KArgs<BATCH>)&A, p0 + j);
     }
 }
 
