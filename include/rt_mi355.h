@@ -481,6 +481,11 @@ float rt_spec_threshold(void);
  * depth-first, one entry a step (csrc/coop.h) — a small n exercises that
  * mode (same answers either way). */
 #define RT_DEBUG_SAMPLE_WAVE_STACK 6
+/* Diagnostics: rt_debug_read(ctx, RT_DEBUG_COUNTERS, out, cap, &n) writes the
+ * 16 64-bit counter words of the last synchronous frame or rt_finish (words
+ * 0-8: rt_stats' counts; word 9: in a -DRT_FETCH_COUNT measuring build, the
+ * bytes those frames' traversal and shading requested; 0 otherwise). */
+#define RT_DEBUG_COUNTERS 7
 int rt_debug_set(rt_ctx *ctx, int32_t what, int32_t value);
 int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, int64_t *bytes_written);
 

@@ -41,6 +41,7 @@ RT_DEBUG_GROUP_SAMPLE_WAVES = 3
 RT_DEBUG_HOST_WAITS = 4
 RT_DEBUG_LAST_LAUNCH = 5
 RT_DEBUG_SAMPLE_WAVE_STACK = 6
+RT_DEBUG_COUNTERS = 7
 RT_BUILD_SAH_HOST = 0
 RT_BUILD_LBVH_GPU = 1
 RT_BUILD_LBVH_GPU_BVH2 = 2

@@ -90,10 +90,12 @@ template <bool ANY, bool COUNT>
 __device__ __forceinline__ void packet_leaf_tris(const rtd::SceneDev &S, const RayCtx &r, PacketLane &L, int &wgate,
                                                  float d2, int first, int count, Counts &cnt) {
     const rtd::TriRec *tb = S.tris + first;
+    RT_FETCH_WAVE(cnt, 48 * count);
     const rtd::TriRec t0 = rtt::cload(tb);
     const rtd::TriRec t1 = rtt::cload(tb + (count > 1 ? 1 : 0));
     const int gate = uni(__float_as_int(t0.p2.z));
     if (gate >= 0 && gate != wgate) {
+        RT_FETCH_WAVE(cnt, 32);
         const rtd::MeshGate g = rtt::cload(S.gates + gate);
         if (L.live) {
             L.gate_ok = rtm::ref_slab(r.o, r.inv(), mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
@@ -359,6 +361,7 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
         if (!ANY && node >= kCutMark) {
             // a waiting cut entry (cut_select): visited only if a live lane's
             // ray still enters its box before the lane's closest hit so far
+            RT_FETCH_WAVE(cnt, 32);
             const rtd::CutBox b = rtt::cload(S.cut->box + (node - kCutMark));
             const int ref = __float_as_int(b.lo.w);
             float k = INFINITY;
@@ -377,6 +380,7 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
         if (node >= 0) L.nodes++; else L.leaves++;
 #endif
         if (node >= 0) {
+            RT_FETCH_WAVE(cnt, 128);
             float k0 = INFINITY, k1 = INFINITY, k2 = INFINITY, k3 = INFINITY;
             const int4 ch = rtt::cload(&S.nodes4[node].child);
             if (same_signs) {

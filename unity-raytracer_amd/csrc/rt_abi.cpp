@@ -184,6 +184,7 @@ int rt_finish(rt_ctx *ctx, rt_stats *stats) {
         for (int w = 0; w < rtd::kCounterWords; ++w) sum[w] += c[w];
         kms = std::max(kms, ms);
     }
+    std::memcpy(ctx->last_counts, sum, sizeof sum);
     if (stats) {
         const double wall =
             t0_set ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() : 0.0;
@@ -440,6 +441,13 @@ int rt_debug_read(rt_ctx *ctx, int32_t what, void *out, int64_t capacity_bytes, 
         return RT_OK;
     }
     if (!ctx) return RT_E_INVALID;
+    if (what == RT_DEBUG_COUNTERS) {
+        if (!out || capacity_bytes <= 0) return fail(ctx, RT_E_INVALID, "rt_debug_read: no output");
+        const int64_t n = std::min<int64_t>(capacity_bytes, (int64_t)sizeof ctx->last_counts);
+        std::memcpy(out, ctx->last_counts, (size_t)n);
+        if (bytes_written) *bytes_written = n;
+        return RT_OK;
+    }
     if (what == RT_DEBUG_LAST_LAUNCH) {
         if (!out || capacity_bytes <= 0) return fail(ctx, RT_E_INVALID, "rt_debug_read: no output");
         const std::string &r = ctx->last_launch;

@@ -592,12 +592,13 @@ int lpt_prepare(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, bool
         ctx->last_lpt = b;
     }
     if (levels && !(F.max_bounces > rtd::kMaxBounces)) {
-        // the levels kernel dispatches XCD-aware stripes in row order
-        // (trace_levels.hip): no longest-first order.  Its 16-spp instance
-        // (the one with the sky test) measures which tiles are sky, and whole
-        // frames in flight leave those to sky_batch_kernel: its positions are
-        // the non-sky tiles in row order (C4 all-sky frames cost 0.955 ms in
-        // flight as a wave per tile; skycost, r05z).
+        // the levels kernel dispatches XCD-aware stripes (trace_levels.hip)
+        // in row order, without splits.  Its 16-spp instance (the one with
+        // the sky test) measures which tiles are sky, and whole frames in
+        // flight leave those to sky_batch_kernel: its positions are then the
+        // measured non-sky tiles, longest first (trace_levels.hip kLvRowKeys:
+        // or in row order) (C4 all-sky frames cost 0.955 ms in flight as a
+        // wave per tile; skycost, r05z).
         if (F.spp == 16 && rtk::kSkyBatch > 1) {
             if (F.tile_order && !count && overlapped_frame(ctx, prm))
                 F.sky_batch_tiles = std::max(0, std::min(ls->sky_tail, F.num_tiles - 1));
@@ -804,8 +805,15 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         if (st) return st;
     }
     // rt_render into a host Color[]: the frame in row slabs, each copied to the
-    // host while the next ones render (the PCIe copy is the longer part)
-    const bool slabs = host_out && out_bytes && F.band_count == 1 && !P.wavefront;
+    // host while the next ones render (the PCIe copy is the longer part) —
+    // copy-bound formats (float RGBA / RGB) of 2 MB or more; the others go
+    // in one piece, copied by this thread right behind the launch on the
+    // same stream (no copier hand-off)
+    const bool copy_bound = F.out_format == rtd::kOutFloat4 || F.out_format == rtd::kOutRGB32F;
+    bool slabs = host_out && out_bytes && F.band_count == 1 && !P.wavefront && copy_bound && out_bytes >= kSlabMinFrame;
+#ifdef RT_EXP_SLAB_WEIGHTS
+    slabs = host_out && out_bytes && F.band_count == 1 && !P.wavefront;  // measuring builds: the weights below
+#endif
     struct Launch {
         rtd::FrameDev F;
         LptSlot *ls;
@@ -827,7 +835,6 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         row_bytes = (int)(out_bytes / (size_t)std::max(1, F.local_rows));
         double wts[kMaxSlabs];
         for (int k = 0; k < kMaxSlabs; ++k) wts[k] = 1.0;
-        const bool copy_bound = F.out_format == rtd::kOutFloat4 || F.out_format == rtd::kOutRGB32F;
         int nslab = out_bytes < kSlabMinFrame || !copy_bound ? 1 : 6;
         if (nslab > 1)
             for (int k = 0; k < nslab; ++k) wts[k] = kSlabsCopyBound[k];
@@ -955,18 +962,21 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             return RT_OK;
         }
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+        // the host copy right behind the launch (the counters' fold and a
+        // re-sort follow it, off the frame's critical path)
+        if (host_out && out_bytes)
+            HIP_WAIT(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
         st = fold_counters(ctx, ctx->stream);
         if (st) return st;
         if (L.sort) {  // after the timed region: the order of the next frames
             st = lpt_sort_now(ctx, L.F, L.ls);
             if (st) return st;
         }
-        if (host_out && out_bytes)
-            HIP_WAIT(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     unsigned long long counts[rtd::kCounterWords];
     read_folded(ctx, counts);
+    std::memcpy(ctx->last_counts, counts, sizeof counts);
     if (stats) {
         float ms = 0.0f;
         HIP_OR_FAIL(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));

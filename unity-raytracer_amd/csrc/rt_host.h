@@ -388,7 +388,8 @@ struct rt_ctx {
     std::atomic<bool> destroying{false};  // rt_destroy has begun (host_waits_report skips the context)
     std::string last_launch;
     std::string last_lpt;  // the longest-first slot's state of the last launch (RT_DEBUG_LAST_LAUNCH)
-    long long sky_waits = 0;  // host waits for a first sort's sky-tail count (lpt_sort_now; RT_DEBUG_LAST_LAUNCH)
+    long long sky_waits = 0;
+    unsigned long long last_counts[rtd::kCounterWords] = {0};  // rt_debug_read RT_DEBUG_COUNTERS  // host waits for a first sort's sky-tail count (lpt_sort_now; RT_DEBUG_LAST_LAUNCH)
     rti::GrowBuf wave_clock;
     int64_t wave_clock_bytes = 0;
 };

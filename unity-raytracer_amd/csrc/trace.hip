@@ -61,8 +61,10 @@ struct SegClock {
 template <bool COUNT, bool MOOT = false>
 __device__ __forceinline__ f3 shade_hit(const SceneDev &S, const rts::Surface &sf, const rtt::Stack &st,
                                         Counts &cnt) {
+    RT_FETCH_LANE(cnt, 64);  // the material (the surface's 16-B record: rts::surface's caller)
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
+        RT_FETCH_WAVE(cnt, 32);
         const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
         cnt.shadow++;
         rtt::RayCtx rs;
@@ -197,6 +199,7 @@ __device__ __forceinline__ f3 shade_levels(const SceneDev &S, const FrameDev &F,
             break;
         }
         if (COUNT) cnt.shading++;
+        RT_FETCH_LANE(cnt, 16);
         const rts::Surface sf = rts::surface(S, o, d, bt, br);
         if (DEEP && depth - depth0 == kMaxBounces && S.mats[sf.mat].ka_mirror.w != 0.0f && depth < F.max_bounces) {
             return deep_chain<COUNT>(S, F, o0, d0, depth0, o, d, st, cnt);
@@ -254,9 +257,11 @@ __device__ __forceinline__ f3 shade_path(const SceneDev &S, const FrameDev &F, f
     int *const hints = HINT && F.shadow_hint ? F.shadow_hint + (size_t)tile * kHintLights : nullptr;
     int4 hv = make_int4(0, 0, 0, 0);
     if (HINT && hints) hv = rtt::cload(reinterpret_cast<const int4 *>(hints));
+    RT_FETCH_LANE(cnt, 16 + 64);  // the hit's shading record and material
     rts::Surface sf = rts::surface(S, o, d, P.best_t, P.best_rank);
     f3 col = rts::ambient(S, S.mats[sf.mat]);
     for (int l = 0; l < S.num_lights; ++l) {  // :327-356
+        RT_FETCH_WAVE(cnt, 32);
         const rts::ShadowRay sr = rts::shadow_ray(sf, S.lights[l]);
         // a moot shadow ray (shade.h same_bits) is not traced
         f3 lit = col + rts::light_term(S, sf, S.mats[sf.mat], S.lights[l], sr);
@@ -365,6 +370,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     // the cut entries do not depend on the tile: their loads are issued first
     rtp::CutLane cl;
     if (!COUNT) cl = rtp::cut_load(S);
+    if (!COUNT && S.cut) RT_FETCH_WAVE(cnt, 7 * 4 * kCutMax + 4);  // the cut table's SoA entries and count
     int px, ly, gy, s;
 #ifdef RT_EXP_ONESAMPLE
     // measuring builds only (wrong images): a sixteenth-wave traces its pixel's first sample alone
@@ -725,6 +731,7 @@ __device__ __forceinline__ void render_wave(const SceneDev &S, const FrameDev &F
     int tile = idx;
     if (F.tile_order) tile = rtt::cload(F.tile_order + idx);
     tile = __builtin_amdgcn_readfirstlane(tile);
+    if (F.tile_order) RT_FETCH_WAVE(cnt, 4);
     // a batch: the frame of the batch tile and its tile within the frame
     int ftile = tile;
     const FrameDev &FF = BATCH ? batch_frame(*B, tile, ftile) : F;
@@ -793,6 +800,12 @@ __device__ __forceinline__ void render_wave(const SceneDev &S, const FrameDev &F
         if (lane_e == 0) F.wave_counts[wid] = make_uint4(sh, rf, mo, F.count_tag);
     } else {
         rtt::flush_counts<COUNT>(cnt, F.counters);
+    }
+#endif
+#ifdef RT_FETCH_COUNT
+    {  // measuring builds: the wave's fetched bytes into counter word 9
+        const unsigned fb = rtt::wave_sum(cnt.fetch);
+        if (lane_e == 0 && fb) atomicAdd(rtt::counter_slot(F.counters) + 9, (unsigned long long)fb);
     }
 #endif
 }
@@ -874,8 +887,15 @@ __device__ __forceinline__ const FrameDev &head(const FrameBatch &B) { return B.
 // ROCm 7.2 compiles it from unrelated SGPRs, which faulted on the GPU.)
 template <bool BATCH>
 using KArgs = const __attribute__((address_space(4))) SkyArgs<BATCH> *;
+// (measuring builds inline it: ROCm 7.2's backend fails on the out-of-line
+// instrumented copy, "V_CMP_NE_U32_e32 0, $src_private_base")
+#ifdef RT_FETCH_COUNT
+#define RT_FALLBACK_LINKAGE __forceinline__
+#else
+#define RT_FALLBACK_LINKAGE __noinline__
+#endif
 template <bool Q4, bool BATCH>
-__device__ __noinline__ void sky_fallback(KArgs<BATCH> pa, int pos) {
+__device__ RT_FALLBACK_LINKAGE void sky_fallback(KArgs<BATCH> pa, int pos) {
     constexpr int FX = Q4 ? 2 : 0;
     const SkyArgs<BATCH> &A = *(const SkyArgs<BATCH> *)pa;
     const SceneDev &S = A.S;
@@ -910,6 +930,10 @@ __device__ __noinline__ void sky_fallback(KArgs<BATCH> pa, int pos) {
     if (H.tile_cost && rtt::lane_id() == 0)
         H.tile_cost[tile] = max(1u, tile_cost_key(__builtin_amdgcn_s_memtime() - t0, -1, 4));
     rtt::flush_counts<false>(cnt, H.counters);
+#ifdef RT_FETCH_COUNT
+    const unsigned fb = rtt::wave_sum(cnt.fetch);
+    if (rtt::lane_id() == 0 && fb) atomicAdd(rtt::counter_slot(H.counters) + 9, (unsigned long long)fb);
+#endif
 }
 
 // The work a frame in flight has after its render_kernel / levels launch, in
@@ -935,6 +959,9 @@ __device__ __forceinline__ void sky_batch_wave(const SkyArgs<BATCH> &A) {
     const int p0 = H.num_tiles - H.sky_batch_tiles + (int)blockIdx.x * rtk::kSkyBatch;
     const int n = min(rtk::kSkyBatch, H.num_tiles - p0);  // wave-uniform
     unsigned stale = 0u;                                 // wave-uniform: bit j, position p0 + j is not sky
+#ifdef RT_FETCH_COUNT
+    if (rtt::lane_id() == 0) atomicAdd(rtt::counter_slot(H.counters) + 9, (unsigned long long)(4 * n));  // the tile indices
+#endif
     for (int j = 0; j < n; ++j) {
         const int tile = __builtin_amdgcn_readfirstlane(rtt::cload(H.tile_order + p0 + j));
         int ftile = tile;

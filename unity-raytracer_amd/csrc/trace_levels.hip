@@ -22,6 +22,15 @@ using rtt::Counts;
 
 namespace {
 
+// The 16-spp order's non-sky tiles: keyed by their measured cost (longest
+// first; default) or all keyed 1 (row order under the stable sort, the XCD
+// stripes' locality kept; measuring builds -DRT_EXP_LVROWKEY=1).
+#ifdef RT_EXP_LVROWKEY
+constexpr bool kLvRowKeys = RT_EXP_LVROWKEY != 0;
+#else
+constexpr bool kLvRowKeys = false;
+#endif
+
 // Waves per SIMD the register budget must allow: 6 (80 VGPRs, fewer spills in
 // the level loop) for up to 16 spp, 7 (72 VGPRs) above (8 until round 5).  Measured (round 3,
 // interleaved A/B): C4 (16 spp, depth 8) 6 waves -5 % single frame / -8 %
@@ -120,12 +129,15 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     }
     const int wid = ((int)q * 8 + (blockIdx.x & 7)) * zs + rk;  // the tile itself
     // positions: the frame's tiles in row order, or (F.tile_order: whole 16-spp
-    // frames in flight) the last measurement's non-sky tiles in row order — the
-    // sky tail is trace.hip sky_batch_kernel's, and the stripes above keep
-    // their locality over the compacted positions
+    // frames in flight) the last measurement's non-sky tiles — longest first
+    // (their measured cost keys), or in row order with kLvRowKeys (every
+    // non-sky tile keyed 1: the stable sort keeps row order, so the stripes
+    // above keep their locality over the compacted positions) — the sky tail
+    // is trace.hip sky_batch_kernel's
     if (wid >= F.num_tiles - F.sky_batch_tiles) return;  // wave-uniform (the last stripes' padding)
     // the tile index in an SGPR (scalar slot -> pixel math, nothing spilled)
     int tile = __builtin_amdgcn_readfirstlane(F.tile_order ? rtt::cload(F.tile_order + wid) : wid);
+    if (F.tile_order) RT_FETCH_WAVE(cnt, 4);
     const unsigned long long t0 = F.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     RT_LSEG(const unsigned long long ts0 = __builtin_amdgcn_s_memtime();
             unsigned long long sg_cam = 0, sg_sh = 0, sg_mir = 0, sg_setup = 0;)
@@ -164,6 +176,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     rtp::CutStart cs = {0, 0, 0, -1};
     if (CUT && F.cut_test && __ballot(alive) != 0) {  // every lane executes here
         const rtp::CutLane cl = rtp::cut_load(S);
+        RT_FETCH_WAVE(cnt, 7 * 4 * kCutMax + 4);  // the cut table's SoA entries and count
         cs = rtp::cut_select(S, F, rts::tile_rect<FIX>(F, tile), wstack_mem, &cl);
     }
     RT_LSEG(sg_setup = __builtin_amdgcn_s_memtime() - ts0;)
@@ -183,6 +196,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         f3 col = mk(0.0f, 0.0f, 0.0f);
         int mat = 0;
         if (hit) {
+            RT_FETCH_LANE(cnt, 16 + 64);  // the hit's shading record and material
             sf = rts::surface(S, o, d, P.best_t, P.best_rank);
             mat = sf.mat;
             col = rts::ambient(S, S.mats[mat]);
@@ -191,6 +205,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
             sf.mat = 0;
         }
         for (int l = 0; l < S.num_lights; ++l) {  // :327-356, wave-uniform
+            RT_FETCH_WAVE(cnt, 32);
             const DevLight Lt = S.lights[l];
             const rts::ShadowRay sr = rts::shadow_ray(sf, Lt);
             if (hit) cnt.shadow++;
@@ -289,7 +304,9 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     if (F.tile_cost && lane2 == 0) {  // (16 spp: the sky flag is what the order is for)
         const unsigned c = (unsigned)min(__builtin_amdgcn_s_memtime() - t0, 0xffffffffull);
         const unsigned e = c ? 31u - __clz(c) : 0u;
-        F.tile_cost[tile] = sky_wave ? 0u : max(1u, e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u)));
+        F.tile_cost[tile] = sky_wave ? 0u
+                            : kLvRowKeys ? 1u
+                                         : max(1u, e < 4 ? c : (((e - 3u) << 4) | ((c >> (e - 4u)) & 15u)));
     }
 #ifdef RT_SEG_PROFILE
     if (lane2 == 0) {  // the clocks are wave-uniform
@@ -314,6 +331,12 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
     } else {
         rtt::flush_counts<false>(cnt, F.counters);
     }
+#ifdef RT_FETCH_COUNT
+    {  // measuring builds: the wave's fetched bytes into counter word 9 (traverse.h RT_FETCH_*)
+        const unsigned fb = rtt::wave_sum(cnt.fetch);
+        if (lane2 == 0 && fb) atomicAdd(rtt::counter_slot(F.counters) + 9, (unsigned long long)fb);
+    }
+#endif
 }
 
 }  // namespace

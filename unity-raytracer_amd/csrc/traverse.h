@@ -24,7 +24,31 @@ struct Counts {
     unsigned primary, shadow, reflection, box, tri, sph, shading;
     unsigned scene_miss;  // camera samples rejected by the scene AABB gate (Scene.cs:54), COUNT launches
     unsigned moot;        // shadow rays whose answer cannot change the colour: not traced (shade.h same_bits)
+#ifdef RT_FETCH_COUNT
+    unsigned fetch;       // measuring builds: bytes requested (RT_FETCH_*)
+#endif
 };
+
+// Measuring builds (-DRT_FETCH_COUNT, lib/variants/fetch; tools/fetch_bytes.py,
+// bench.py roofline.fetched_bytes_per_launch): the bytes a frame's traversal
+// and shading request from the cache hierarchy — a node (128 B), triangle
+// (48 B), sphere (32 B) or mesh-gate (32 B) record, a cut box (32 B), the cut
+// table (1,796 B), a shading record (16 B), a material (64 B), a light (32 B),
+// a tile index (4 B).  A wave-uniform fetch (a packet's scalar loads) counts
+// once per wave (RT_FETCH_WAVE: by its first active lane), a per-lane fetch
+// once per lane (RT_FETCH_LANE).  The product build compiles none of it.
+#ifdef RT_FETCH_COUNT
+__device__ __forceinline__ bool fetch_lead() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l == __ffsll((long long)__ballot(1)) - 1;
+}
+#define RT_FETCH_LANE(c, n) ((c).fetch += (unsigned)(n))
+#define RT_FETCH_WAVE(c, n) ((c).fetch += rtt::fetch_lead() ? (unsigned)(n) : 0u)
+#else
+#define RT_FETCH_LANE(c, n) ((void)0)
+#define RT_FETCH_WAVE(c, n) ((void)0)
+#endif
 
 __device__ __forceinline__ float nudge(float v) { return fabsf(v) > 1e-20f ? v : copysignf(1e-20f, v); }
 
@@ -156,9 +180,12 @@ __device__ __forceinline__ bool leaf(const rtd::SceneDev &S, const RayCtx &r, Tr
             const rtd::MeshGate g = S.gates[gate];
             t.gate_ok = rtm::ref_slab(r.o, r.inv(), mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
             if (COUNT) cnt.box++;
+            if (UNIFORM) RT_FETCH_WAVE(cnt, 32); else RT_FETCH_LANE(cnt, 32);
         }
         if (!t.gate_ok) return false;
     }
+    if (UNIFORM) RT_FETCH_WAVE(cnt, (kind == rtd::kLeafTri ? 48 : 32) * count);
+    else RT_FETCH_LANE(cnt, (kind == rtd::kLeafTri ? 48 : 32) * count);
     if (kind == rtd::kLeafTri) {
         for (int i = 0; i < count; ++i) {
             const rtd::TriRec tr = UNIFORM ? cload(S.tris + first + i) : S.tris[first + i];
@@ -235,6 +262,7 @@ __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const 
     const rtd::TriRec t0 = b[0];
     const rtd::TriRec t1 = b[count > 1 ? 1 : 0];
     const int gate = __float_as_int(t0.p2.z);
+    RT_FETCH_LANE(cnt, 48 * (count > 2 ? 2 : count));
     if (MESH_ONLY && gate < 0) return false;  // a loose-triangle leaf (leaves are homogeneous in mesh)
     if (gate >= 0) {
         if (gate != t.gate_cached) {
@@ -242,12 +270,14 @@ __device__ __forceinline__ bool leaf_tris_batched(const rtd::SceneDev &S, const 
             const rtd::MeshGate g = S.gates[gate];
             t.gate_ok = rtm::ref_slab(r.o, r.inv(), mk(g.lo.x, g.lo.y, g.lo.z), mk(g.hi.x, g.hi.y, g.hi.z));
             if (COUNT) cnt.box++;
+            RT_FETCH_LANE(cnt, 32);
         }
         if (!t.gate_ok) return false;
     }
     if (tri_rec<ANY, COUNT>(r, t, d2, t0, cnt)) return true;
     if (count > 1 && tri_rec<ANY, COUNT>(r, t, d2, t1, cnt)) return true;
     if (count > 2) {  // the second pair, fetched together after the first
+        RT_FETCH_LANE(cnt, 48 * (count - 2));
         const rtd::TriRec t2 = b[2];
         const rtd::TriRec t3 = b[count > 3 ? 3 : 2];
         if (tri_rec<ANY, COUNT>(r, t, d2, t2, cnt)) return true;
@@ -324,6 +354,7 @@ template <bool ANY, bool COUNT, bool MESH_ONLY = false>
 __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &r, Trav &t, float d2,
                                           const Stack &st, Counts &cnt) {
     if (t.node >= 0 && S.bvh4) {
+        RT_FETCH_LANE(cnt, 128);
         const rtd::BvhNode4 *np = S.nodes4 + t.node;
         const float4 lx = np->lox, hx = np->hix, ly = np->loy, hy = np->hiy, lz = np->loz, hz = np->hiz;
         const int4 ch = np->child;
@@ -367,6 +398,7 @@ __device__ __forceinline__ bool trav_step(const rtd::SceneDev &S, const RayCtx &
             return false;
         }
     } else if (t.node >= 0) {
+        RT_FETCH_LANE(cnt, 64);
         const rtd::BvhNode *np = S.nodes + t.node;
         const float4 a = np->a, b = np->b, c = np->c;
         const int4 ch = np->d;

@@ -221,6 +221,16 @@ class Context:
                                                     C.c_void_p(dev_ptr), C.c_size_t(stride), C.byref(stats)))
         return stats
 
+    def counter_words(self):
+        """rt_debug_read(RT_DEBUG_COUNTERS): the 16 counter words of the last
+        synchronous frame or rt_finish (word 9: fetched bytes, measuring
+        builds)."""
+        buf = (C.c_uint64 * 16)()
+        n = C.c_int64(0)
+        self._check(self.lib.rt_debug_read(self.h, abi.RT_DEBUG_COUNTERS, C.cast(buf, C.c_void_p), C.sizeof(buf),
+                                           C.byref(n)))
+        return list(buf)
+
     def finish(self) -> abi.rt_stats:
         """Wait for RT_FLAG_ASYNC frames; their summed stats."""
         stats = abi.rt_stats()
