@@ -81,6 +81,18 @@ if has drv; then
     || fail drv200 $out/drv200_$tag.log
   tail -1 $out/drv200_$tag.log | cut -c1-400
 fi
+if has focus; then
+  # the tests of what changed last (FOCUS: a pytest -k expression), before the whole suite
+  timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${FOCUS:?FOCUS}" \
+    > $out/focus_$tag.log 2>&1 || fail focus $out/focus_$tag.log 40
+  tail -1 $out/focus_$tag.log
+fi
+if has fetch; then
+  # fetched bytes per frame of the timed path (the RT_FETCH_COUNT measuring build)
+  timeout -k 10 300 python -u tools/fetch_bytes.py > $out/fetch_$tag.log 2>&1 || fail fetch $out/fetch_$tag.log
+  cp profiles/canonical_counts.json $out/canonical_counts_$tag.json
+  cat $out/fetch_$tag.log | cut -c1-300
+fi
 if has kt; then
   cd /tmp
   # the bench's timed frames (no moving camera: the in-flight instance's last 50 launches are the timed
