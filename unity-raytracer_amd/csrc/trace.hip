@@ -356,6 +356,24 @@ constexpr int kMkWaves = 1;
 constexpr int kMkThreads = kMkWaves * kWaveSize;
 
 
+// The frame block (a kernel argument) through an opaque copy of its address:
+// the fields read after a tile's trace are loaded there (scalar loads) rather
+// than loaded at kernel entry and kept live — in SGPRs, spilled — across the
+// packet loops (measuring builds: -DRT_EXP_LAUNDER).
+#ifdef RT_EXP_LAUNDER
+constexpr bool kLaunder = true;
+#else
+constexpr bool kLaunder = false;
+#endif
+template <typename T>
+__device__ __forceinline__ const T &reload_arg(const T &x) {
+    if (!kLaunder) return x;
+    typedef const __attribute__((address_space(4))) T KT;
+    KT *p = (KT *)&x;
+    asm volatile("" : "+s"(p));
+    return *(const T *)p;
+}
+
 // One tile (a wave) of the megakernel: trace every sample, sum a pixel's
 // samples in row-major sample order ((s0 + s1) + s2) + ..., store.
 // part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
@@ -406,7 +424,8 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
             color = shade_path<COUNT, DEEP, HINT, MOOT>(S, F, o, d, st, wstack, cnt, sg, cs, tile);
         }
     }
-    const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
+    const FrameDev &FE = reload_arg(F);
+    const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : FE.spp);
     // the slot -> pixel mapping is recomputed from the (scalar) tile index and
     // the lane id (v_mbcnt, opaque to the compiler so it is not kept live)
     // rather than kept live across the trace, where it would be spilled
@@ -414,19 +433,19 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     asm volatile("" : "+s"(tile2));
     const int lane2 = rtt::lane_id();
     const bool active2 =
-        rts::slot_pixel<Q4 ? 2 : 0>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
-    if (HINT && !COUNT && pshift == 0 && (Q4 || F.spp == 4)) {
+        rts::slot_pixel<Q4 ? 2 : 0>(FE, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
+    if (HINT && !COUNT && pshift == 0 && (Q4 || FE.spp == 4)) {
         // a one-sample wave of a split pixel: its sample goes to the pixel's
         // slots by write-through (sc1) stores, then the pixel's arrival count;
         // the fourth arrival sums the samples in sample order, as sample_sum
         if (active2) {
             typedef __attribute__((address_space(1))) unsigned gu32;
             typedef __attribute__((address_space(1))) int gi32;
-            float *sp = F.split_samples + ((size_t)sidx * kWaveSize + lane2) * 4;
+            float *sp = FE.split_samples + ((size_t)sidx * kWaveSize + lane2) * 4;
             __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int *cp = F.split_count + sidx * (kWaveSize / 4) + (lane2 >> 2);
+            int *cp = FE.split_count + sidx * (kWaveSize / 4) + (lane2 >> 2);
 #ifdef RT_EXP_RELACQ
             // measuring builds: the C++ memory model's release / acquire pair
             if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == 3) {
@@ -442,14 +461,14 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
             if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
 #endif
-                const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (lane2 & ~3)) * 4;
+                const float *b = FE.split_samples + ((size_t)sidx * kWaveSize + (lane2 & ~3)) * 4;
                 auto ld = [](const float *q) {
                     return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 };
                 f3 v = mk(ld(b), ld(b + 1), ld(b + 2));
                 for (int k = 1; k < 4; ++k) v = v + mk(ld(b + 4 * k), ld(b + 4 * k + 1), ld(b + 4 * k + 2));
                 v = v * 0.25f;
-                rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+                rts::store_pixel(FE, (size_t)ly * FE.res_x + px, v);
                 __hip_atomic_store((gi32 *)cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
             }
         }
@@ -459,9 +478,9 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
         f3 v = sum;
         if (Q4)
             v = v * 0.25f;  // == v / 4: the same real number, rounded once
-        else if (F.spp > 1)
-            v = (F.spp & (F.spp - 1)) == 0 ? v * F.inv_spp : v / (float)F.spp;  // likewise for 2^k
-        rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
+        else if (FE.spp > 1)
+            v = (FE.spp & (FE.spp - 1)) == 0 ? v * FE.inv_spp : v / (float)FE.spp;  // likewise for 2^k
+        rts::store_pixel(FE, (size_t)ly * FE.res_x + px, v);
     }
     return sky;
 }
@@ -863,16 +882,7 @@ __device__ __forceinline__ void wave_counts_part(const FrameDev &F, int waves, i
     }
 }
 
-// A tile of a sky tail that is not sky this frame (the order predates a
-// camera or scene change): rendered in full, as render_kernel's whole-frame
-// instance would, after the sky loop (sky_batch_wave) — which keeps only its
-// loop state live, not the tile path's frame constants (with render_tile
-// inside the sky loop the kernel had 152 VGPR / 163 SGPR spill slots and wrote
-// 1.6x its sky pixels, round 5).  The tallies go to the counters directly.
-// pos: the tile's position in the order.
-// The sky kernels' one argument: its kernel-argument segment is this block,
-// which the out-of-line fallback reads through the segment pointer (scalar
-// loads; a callee's pointer arguments would arrive in VGPRs).
+// The sky kernels' argument block: the scene, the frame (or the batch) and the grid split.
 template <bool BATCH>
 struct SkyArgs {
     SceneDev S;
@@ -881,32 +891,36 @@ struct SkyArgs {
 };
 __device__ __forceinline__ const FrameDev &head(const FrameDev &F) { return F; }
 __device__ __forceinline__ const FrameDev &head(const FrameBatch &B) { return B.f[0]; }
-// (The argument block arrives as a pointer argument, i.e. in VGPRs, so the
-// loads of its fields here are vector loads: a rare path.  Not the kernarg
-// segment pointer builtin: a callee does not receive the segment pointer —
-// ROCm 7.2 compiles it from unrelated SGPRs, which faulted on the GPU.)
-template <bool BATCH>
-using KArgs = const __attribute__((address_space(4))) SkyArgs<BATCH> *;
-// (measuring builds inline it: ROCm 7.2's backend fails on the out-of-line
-// instrumented copy, "V_CMP_NE_U32_e32 0, $src_private_base")
-#ifdef RT_FETCH_COUNT
-#define RT_FALLBACK_LINKAGE __forceinline__
-#else
-#define RT_FALLBACK_LINKAGE __noinline__
-#endif
+// The frame of tile t of the argument block's frame or batch (and the tile in
+// it).  (No pointer cast between the two: a cast of the by-value argument
+// makes the compiler copy the whole block into scratch at kernel entry.)
+__device__ __forceinline__ const FrameDev &frame_of(const FrameDev &F, int t, int &tile) {
+    tile = t;
+    return F;
+}
+__device__ __forceinline__ const FrameDev &frame_of(const FrameBatch &B, int t, int &tile) {
+    return batch_frame(B, t, tile);
+}
+// A tile of a sky tail that is not sky this frame (the order predates a
+// camera or scene change): rendered in full by the per-lane Whitted loop
+// (shade_levels, the mirror chains' path: the same answers as render_tile's
+// packets, bit for bit, with a fraction of its registers), after the sky loop
+// (sky_batch_wave), which so keeps only its own state live — with render_tile
+// inside the sky loop the kernel had 152 VGPR / 163 SGPR spill slots and wrote
+// 1.6x its sky pixels (round 5).  Not out of line: ROCm 7.2 miscompiles a
+// callee's generic pointers to its private overflow stack (a GPU fault on the
+// first stale tile, r07b/r07d; an "Illegal instruction ... src_private_base"
+// compile error in other forms).  The tallies go to the counters directly.
+// pos: the tile's position in the order.
 template <bool Q4, bool BATCH>
-__device__ RT_FALLBACK_LINKAGE void sky_fallback(KArgs<BATCH> pa, int pos) {
+__device__ __forceinline__ void sky_fallback(const SkyArgs<BATCH> &A, const rtt::Stack &st, int pos) {
     constexpr int FX = Q4 ? 2 : 0;
-    const SkyArgs<BATCH> &A = *(const SkyArgs<BATCH> *)pa;
     const SceneDev &S = A.S;
     const FrameDev &H = head(A.P);
-    __shared__ int stack_mem[kStackSize * kWaveSize];
-    int ovf[kStackTotal - kStackSize];
-    const rtt::Stack st{stack_mem, ovf, kStackSize};  // (+ lane per query: traverse)
     Counts cnt = {0, 0, 0, 0, 0, 0, 0};
     const int tile = __builtin_amdgcn_readfirstlane(rtt::cload(H.tile_order + pos));
     int ftile = tile;
-    const FrameDev &F = BATCH ? batch_frame(*(const FrameBatch *)&A.P, tile, ftile) : H;
+    const FrameDev &F = frame_of(A.P, tile, ftile);
     const unsigned long long t0 = H.tile_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     int px, ly, gy, s;
     const bool active = rts::slot_pixel<FX>(F, ftile, rtt::lane_id(), px, ly, gy, s);
@@ -914,8 +928,6 @@ __device__ RT_FALLBACK_LINKAGE void sky_fallback(KArgs<BATCH> pa, int pos) {
     if (active) {
         f3 o, d;
         rts::primary_ray<FX>(F, px, gy, s, o, d);
-        // the per-lane Whitted loop (shade_levels, the mirror chains' path):
-        // the same answers as render_tile's packets, bit for bit
         color = shade_levels<false, false, true>(S, F, o, d, 0, st, cnt);
     }
     const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
@@ -965,18 +977,24 @@ __device__ __forceinline__ void sky_batch_wave(const SkyArgs<BATCH> &A) {
     for (int j = 0; j < n; ++j) {
         const int tile = __builtin_amdgcn_readfirstlane(rtt::cload(H.tile_order + p0 + j));
         int ftile = tile;
-        const FrameDev &F = BATCH ? batch_frame(*(const FrameBatch *)&A.P, tile, ftile) : H;
+        const FrameDev &F = frame_of(A.P, tile, ftile);
         if (sky_tile<Q4>(F, ftile)) {
             if (H.tile_cost && rtt::lane_id() == 0) H.tile_cost[tile] = 0u;  // still sky: dispatched last again
         } else {
             stale |= 1u << j;
         }
     }
-    while (stale) {  // (rare: a camera or scene change since the order's measurement)
+    if (!stale) return;
+    // (rare: a camera or scene change since the order's measurement) — after
+    // the sky loop, so the loop keeps only its own state live
+    __shared__ int stack_mem[kStackSize * kWaveSize];
+    int ovf[kStackTotal - kStackSize];
+    const rtt::Stack st{stack_mem, ovf, kStackSize};  // (+ lane per query: traverse)
+    do {
         const int j = __builtin_ctz(stale);
         stale &= stale - 1u;
-        sky_fallback<Q4, BATCH>((KArgs<BATCH>)&A, p0 + j);
-    }
+        sky_fallback<Q4, BATCH>(A, st, p0 + j);
+    } while (stale);
 }
 
 template <bool Q4>
