@@ -356,24 +356,6 @@ constexpr int kMkWaves = 1;
 constexpr int kMkThreads = kMkWaves * kWaveSize;
 
 
-// The frame block (a kernel argument) through an opaque copy of its address:
-// the fields read after a tile's trace are loaded there (scalar loads) rather
-// than loaded at kernel entry and kept live — in SGPRs, spilled — across the
-// packet loops (measuring builds: -DRT_EXP_LAUNDER).
-#ifdef RT_EXP_LAUNDER
-constexpr bool kLaunder = true;
-#else
-constexpr bool kLaunder = false;
-#endif
-template <typename T>
-__device__ __forceinline__ const T &reload_arg(const T &x) {
-    if (!kLaunder) return x;
-    typedef const __attribute__((address_space(4))) T KT;
-    KT *p = (KT *)&x;
-    asm volatile("" : "+s"(p));
-    return *(const T *)p;
-}
-
 // One tile (a wave) of the megakernel: trace every sample, sum a pixel's
 // samples in row-major sample order ((s0 + s1) + s2) + ..., store.
 // part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
@@ -424,8 +406,7 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
             color = shade_path<COUNT, DEEP, HINT, MOOT>(S, F, o, d, st, wstack, cnt, sg, cs, tile);
         }
     }
-    const FrameDev &FE = reload_arg(F);
-    const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : FE.spp);
+    const f3 sum = rts::sample_sum(color, rtt::lane_id(), Q4 ? 4 : F.spp);
     // the slot -> pixel mapping is recomputed from the (scalar) tile index and
     // the lane id (v_mbcnt, opaque to the compiler so it is not kept live)
     // rather than kept live across the trace, where it would be spilled
@@ -433,19 +414,19 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     asm volatile("" : "+s"(tile2));
     const int lane2 = rtt::lane_id();
     const bool active2 =
-        rts::slot_pixel<Q4 ? 2 : 0>(FE, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
-    if (HINT && !COUNT && pshift == 0 && (Q4 || FE.spp == 4)) {
+        rts::slot_pixel<Q4 ? 2 : 0>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
+    if (HINT && !COUNT && pshift == 0 && (Q4 || F.spp == 4)) {
         // a one-sample wave of a split pixel: its sample goes to the pixel's
         // slots by write-through (sc1) stores, then the pixel's arrival count;
         // the fourth arrival sums the samples in sample order, as sample_sum
         if (active2) {
             typedef __attribute__((address_space(1))) unsigned gu32;
             typedef __attribute__((address_space(1))) int gi32;
-            float *sp = FE.split_samples + ((size_t)sidx * kWaveSize + lane2) * 4;
+            float *sp = F.split_samples + ((size_t)sidx * kWaveSize + lane2) * 4;
             __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int *cp = FE.split_count + sidx * (kWaveSize / 4) + (lane2 >> 2);
+            int *cp = F.split_count + sidx * (kWaveSize / 4) + (lane2 >> 2);
 #ifdef RT_EXP_RELACQ
             // measuring builds: the C++ memory model's release / acquire pair
             if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == 3) {
@@ -461,14 +442,14 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
             if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
 #endif
-                const float *b = FE.split_samples + ((size_t)sidx * kWaveSize + (lane2 & ~3)) * 4;
+                const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (lane2 & ~3)) * 4;
                 auto ld = [](const float *q) {
                     return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                 };
                 f3 v = mk(ld(b), ld(b + 1), ld(b + 2));
                 for (int k = 1; k < 4; ++k) v = v + mk(ld(b + 4 * k), ld(b + 4 * k + 1), ld(b + 4 * k + 2));
                 v = v * 0.25f;
-                rts::store_pixel(FE, (size_t)ly * FE.res_x + px, v);
+                rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
                 __hip_atomic_store((gi32 *)cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
             }
         }
@@ -478,9 +459,9 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
         f3 v = sum;
         if (Q4)
             v = v * 0.25f;  // == v / 4: the same real number, rounded once
-        else if (FE.spp > 1)
-            v = (FE.spp & (FE.spp - 1)) == 0 ? v * FE.inv_spp : v / (float)FE.spp;  // likewise for 2^k
-        rts::store_pixel(FE, (size_t)ly * FE.res_x + px, v);
+        else if (F.spp > 1)
+            v = (F.spp & (F.spp - 1)) == 0 ? v * F.inv_spp : v / (float)F.spp;  // likewise for 2^k
+        rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
     }
     return sky;
 }
