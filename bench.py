@@ -450,8 +450,10 @@ def main():
     # go as ONE launch (rt_render_device_batch) into the group's buffer, the
     # groups alternate over two streams (two batches in flight); one
     # collective per group as before.
-    batch = args.batch or (4 if (dist_on or args.sim_bands) and band_count > 1 else 1)
-    batch = max(1, min(batch, rt.abi.RT_MAX_BATCH))
+    batch_on = args.batch > 1 or (args.batch == 0 and (dist_on or args.sim_bands) and band_count > 1)
+    # (frames per batch = frames per gather group: --gather-frames, else --batch, else 4)
+    batch = max(1, min(args.gather_frames or (args.batch if args.batch > 1 else 4), rt.abi.RT_MAX_BATCH)) \
+        if batch_on else 1
     # sharded frames travel as float RGB (RT_FLAG_OUT_RGB32F: the Color values
     # bit for bit without the constant alpha, 12 B/px): a quarter less to gather
     ch = 3 if dist_on else 4

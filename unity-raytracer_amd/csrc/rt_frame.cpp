@@ -888,6 +888,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
         if (st) return st;
         launches.push_back(L);
     }
+    bool sync_done = false;  // the frame's work (and its counters' fold) has completed
     const size_t ctr_bytes = rtd::kCounterSlots * rtd::kCounterWords * sizeof(unsigned long long);
     if (!async || ctx->async_frames == 0) {
         // async frames share one set of counters until rt_finish / the next synchronous frame
@@ -962,18 +963,27 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             return RT_OK;
         }
         HIP_OR_FAIL(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-        // the host copy right behind the launch (the counters' fold and a
-        // re-sort follow it, off the frame's critical path)
-        if (host_out && out_bytes)
-            HIP_WAIT(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
-        st = fold_counters(ctx, ctx->stream);
+        st = fold_counters(ctx, ctx->stream);  // (a 256-thread launch into host-mapped words)
         if (st) return st;
-        if (L.sort) {  // after the timed region: the order of the next frames
+        if (host_out && out_bytes) {
+            // the host copy right behind the launch and the counters' fold;
+            // once the stream has drained up to here the frame is complete and
+            // its folded counters readable — a re-sort is enqueued after that,
+            // off the frame's critical path, and not awaited (the next frame on
+            // the stream follows it)
+            HIP_WAIT(ctx, hipMemcpyAsync(host_out, d_out, out_bytes, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));  // (a page-locked host_out: the copy was async)
+            if (L.sort) {
+                st = lpt_sort_now(ctx, L.F, L.ls);
+                if (st) return st;
+            }
+            sync_done = true;
+        } else if (L.sort) {  // after the timed region: the order of the next frames
             st = lpt_sort_now(ctx, L.F, L.ls);
             if (st) return st;
         }
     }
-    HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
+    if (!sync_done) HIP_WAIT(ctx, hipStreamSynchronize(ctx->stream));
     unsigned long long counts[rtd::kCounterWords];
     read_folded(ctx, counts);
     std::memcpy(ctx->last_counts, counts, sizeof counts);
