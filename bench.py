@@ -277,7 +277,7 @@ def cpu_baseline(rt, fr, budget_s, ctx):
                 ts.append(time.perf_counter() - t0)
                 rays_f = c["primary_rays"] + c["shadow_rays"] + c["reflection_rays"]
             med = float(np.median(ts))
-            full[f"{name.lower()}_full" + ("" if nt == 1 else "_all_cores")] = {
+            full[f"{name.lower()}_full" + ("" if nt == 1 else f"_threads_{nt}")] = {
                 "mrays_per_s": rays_f / med / 1e6, "ms_per_frame": med * 1e3, "rays_per_frame": rays_f,
                 "threads": nt, "runs": reps, "frame": f"{ff.plane.ResolutionX}x{ff.plane.ResolutionY}, "
                                                     f"{ff.spp} spp, depth {ff.max_bounces}"}
@@ -289,13 +289,16 @@ def cpu_baseline(rt, fr, budget_s, ctx):
         "sample": f"{pixels} seeded random pixels of {fr.name} ({fr.spp} spp, depth {fr.max_bounces}), "
                   f"{rays} rays in {secs:.1f} s, brute-force C oracle (oracle/rt_oracle.c, gcc -O3 "
                   f"-march=x86-64-v2 -ffp-contract=off), 1 thread (the reference is single-threaded)",
-        "all_cores_value": mrays / msecs / 1e6,
-        "all_cores_threads": threads,
-        "all_cores_sample": f"{mpix} seeded random pixels, {mrays} rays in {msecs:.1f} s",
-        "bvh_all_cores_value": brays / bsecs / 1e6,
-        "bvh_all_cores_sample": f"{bpix} seeded random pixels, {brays} rays in {bsecs:.1f} s, the oracle with a "
-                                f"CPU BVH (median split, leaves <= 4; same answers as the scan), "
-                                f"{threads} threads",
+        f"threads_{threads}_value": mrays / msecs / 1e6,
+        f"threads_{threads}_sample": f"{mpix} seeded random pixels, {mrays} rays in {msecs:.1f} s",
+        # the threads this job may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU pool grants a
+        # one-GPU job 16 CPU threads of the host, whatever nproc says)
+        "threads_used": threads,
+        "threads_why": (f"min(affinity {facts['affinity_cpus']}, OMP_NUM_THREADS {omp}): the pool's CPU share of "
+                        f"a one-GPU job" if omp else f"affinity mask {facts['affinity_cpus']}"),
+        f"bvh_threads_{threads}_value": brays / bsecs / 1e6,
+        f"bvh_threads_{threads}_sample": f"{bpix} seeded random pixels, {brays} rays in {bsecs:.1f} s, the oracle "
+                                         f"with a CPU BVH (median split, leaves <= 4; same answers as the scan)",
         "bvh_same_tree": {"mrays_per_s": srays / ssecs / 1e6, "threads": threads,
                           "sample": f"{spix} seeded random pixels, {srays} rays in {ssecs:.1f} s: the GPU's own "
                                     f"4-wide SAH tree (rt_export_bvh) traversed per ray on the CPU like "
@@ -358,7 +361,7 @@ def main():
                     help="N > 1: frames per RCCL gather (one collective per group of frames; 0 = --streams)")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per launch (rt_render_device_batch: frames of one layout from their own cameras as "
-                         "one launch, their tiles under one longest-first order); 0 = 4 for a rank's row band "
+                         "one launch, their tiles under one longest-first order); 0 = 8 for a rank's row band "
                          "(N > 1 or --sim-bands: each band alone is too small to fill the GPU), 1 otherwise")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--sim-bands", type=int, default=0,
@@ -451,8 +454,9 @@ def main():
     # groups alternate over two streams (two batches in flight); one
     # collective per group as before.
     batch_on = args.batch > 1 or (args.batch == 0 and (dist_on or args.sim_bands) and band_count > 1)
-    # (frames per batch = frames per gather group: --gather-frames, else --batch, else 4)
-    batch = max(1, min(args.gather_frames or (args.batch if args.batch > 1 else 4), rt.abi.RT_MAX_BATCH)) \
+    # (frames per batch = frames per gather group: --gather-frames, else --batch, else 8 — a 1/8 C3 share:
+    # 43.3 Grays/s per rank in batches of 8, 33.7 in 4, 30.3 one frame a launch; r07f)
+    batch = max(1, min(args.gather_frames or (args.batch if args.batch > 1 else 8), rt.abi.RT_MAX_BATCH)) \
         if batch_on else 1
     # sharded frames travel as float RGB (RT_FLAG_OUT_RGB32F: the Color values
     # bit for bit without the constant alpha, 12 B/px): a quarter less to gather

@@ -421,13 +421,19 @@ int record_async_end(rt_ctx *ctx) {
 // True when this frame may run beside another of the context's frames: an
 // RT_FLAG_ASYNC frame while a frame enqueued on another stream is pending
 // (since the last rt_finish), whose tiles then fill the GPU during this
-// frame's tail.  A frame with nothing beside it (synchronous, or async frames
-// on one stream) is its own critical path and splits its slowest tiles.
+// frame's tail — or the first async frame after an rt_finish when the async
+// frame before it ran on another stream: a caller that cycles its frames over
+// several streams enqueues the others right behind it (bench.py's timed
+// frames after its warm-up: as a lone frame that first frame ran the split
+// instance without sky batches, 2.0 ms instead of 0.68 beside the others, and
+// held its stream a frame behind for the rest of a 20-frame window, r07f).
+// A frame with nothing beside it (synchronous, or async frames on one
+// stream) is its own critical path and splits its slowest tiles.
 static bool overlapped_frame(const rt_ctx *ctx, const rt_render_params *prm) {
     if ((prm->flags & RT_FLAG_ASYNC) == 0) return false;
     for (const auto &se : ctx->async_end)
         if (se.first && se.first != ctx->stream) return true;
-    return false;
+    return ctx->async_frames == 0 && ctx->last_async_stream && ctx->last_async_stream != ctx->stream;
 }
 
 // One-sample waves in this frame's band.  The bands of a multi-device frame
@@ -955,6 +961,7 @@ int run_frame(rt_ctx *ctx, rtd::FrameDev &F, const rt_render_params *prm, void *
             }
             st = record_async_end(ctx);
             if (st) return st;
+            ctx->last_async_stream = ctx->stream;
             if (ctx->async_frames++ == 0 && ctx->async_t0_set == false) {
                 ctx->async_t0 = t_start;
                 ctx->async_t0_set = true;

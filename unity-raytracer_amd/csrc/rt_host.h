@@ -365,6 +365,7 @@ struct rt_ctx {
     // end event of the last RT_FLAG_ASYNC frame per stream: rt_finish's device
     // time spans from the first async frame to the last of them to finish
     std::vector<std::pair<hipStream_t, hipEvent_t>> async_end;
+    hipStream_t last_async_stream = nullptr;  // the stream of the last RT_FLAG_ASYNC frame (kept across rt_finish)
     // rt_render's slab pipeline: copy stream + one event per slab
     hipStream_t copy_stream = nullptr;
     rti::Copier copier;  // its thread runs only after a context's first host-output frame

@@ -356,6 +356,50 @@ constexpr int kMkWaves = 1;
 constexpr int kMkThreads = kMkWaves * kWaveSize;
 
 
+// The hand-off of a one-sample wave's sample (a lone shard's finely split
+// pixel, F.s16_shift 0): the sample goes to the pixel's slots, then the
+// pixel's arrival count; the fourth arrival sums the four samples in sample
+// order (as sample_sum) and stores the pixel.  Two forms (A/B: RT_EXP_RELAXED):
+// * release / acquire (the default since round 6): a release fetch-add of the
+//   count and an acquire fence in the last arrival — the C++ memory model's
+//   hand-off, at agent scope (the arrivals run on any XCD);
+// * relaxed (round 5): the samples as agent-scope (write-through) stores, an
+//   explicit wait for them before a relaxed count, agent-scope loads after it
+//   — the same hand-off on gfx950 without the L2 write-back an agent-scope
+//   release costs, but argued from the ISA rather than the memory model.
+#ifdef RT_EXP_RELAXED
+constexpr bool kRelAcqHandoff = false;  // measuring builds only
+#else
+constexpr bool kRelAcqHandoff = true;
+#endif
+__device__ __forceinline__ void split_handoff(const FrameDev &F, int sidx, int slot, f3 color, size_t pixel) {
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    typedef __attribute__((address_space(1))) int gi32;
+    float *sp = F.split_samples + ((size_t)sidx * kWaveSize + slot) * 4;
+    __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int *cp = F.split_count + sidx * (kWaveSize / 4) + (slot >> 2);
+    bool last;
+    if (kRelAcqHandoff) {
+        last = __hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == 3;
+        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
+        last = __hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3;
+    }
+    if (!last) return;
+    const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (slot & ~3)) * 4;
+    auto ld = [](const float *q) {
+        return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    };
+    f3 v = mk(ld(b), ld(b + 1), ld(b + 2));
+    for (int k = 1; k < 4; ++k) v = v + mk(ld(b + 4 * k), ld(b + 4 * k + 1), ld(b + 4 * k + 2));
+    v = v * 0.25f;
+    rts::store_pixel(F, pixel, v);
+    __hip_atomic_store((gi32 *)cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
+}
+
 // One tile (a wave) of the megakernel: trace every sample, sum a pixel's
 // samples in row-major sample order ((s0 + s1) + s2) + ..., store.
 // part >= 0: this wave takes only the lanes l with (l >> pshift) == part:
@@ -416,43 +460,9 @@ __device__ __forceinline__ bool render_tile(const SceneDev &S, const FrameDev &F
     const bool active2 =
         rts::slot_pixel<Q4 ? 2 : 0>(F, tile2, lane2, px, ly, gy, s) && (part < 0 || (lane2 >> pshift) == part);
     if (HINT && !COUNT && pshift == 0 && (Q4 || F.spp == 4)) {
-        // a one-sample wave of a split pixel: its sample goes to the pixel's
-        // slots by write-through (sc1) stores, then the pixel's arrival count;
-        // the fourth arrival sums the samples in sample order, as sample_sum
-        if (active2) {
-            typedef __attribute__((address_space(1))) unsigned gu32;
-            typedef __attribute__((address_space(1))) int gi32;
-            float *sp = F.split_samples + ((size_t)sidx * kWaveSize + lane2) * 4;
-            __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int *cp = F.split_count + sidx * (kWaveSize / 4) + (lane2 >> 2);
-#ifdef RT_EXP_RELACQ
-            // measuring builds: the C++ memory model's release / acquire pair
-            if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT) == 3) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#else
-            // The samples are agent-scope (write-through) stores; waiting for
-            // them before the count makes every one of them reach the device's
-            // coherence point before the count does, and the last arrival's
-            // loads are agent-scope too (they read that point), issued only
-            // after its count returned — the hand-off a release / acquire pair
-            // would give, without the L2 write-back an agent-scope release
-            // costs on gfx950 (A/B: RT_EXP_RELACQ).
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
-            if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
-#endif
-                const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (lane2 & ~3)) * 4;
-                auto ld = [](const float *q) {
-                    return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                };
-                f3 v = mk(ld(b), ld(b + 1), ld(b + 2));
-                for (int k = 1; k < 4; ++k) v = v + mk(ld(b + 4 * k), ld(b + 4 * k + 1), ld(b + 4 * k + 2));
-                v = v * 0.25f;
-                rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
-                __hip_atomic_store((gi32 *)cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
-            }
-        }
+        // a one-sample wave of a split pixel: the hand-off of its sample to
+        // the pixel's last arrival (split_handoff)
+        if (active2) split_handoff(F, sidx, lane2, color, (size_t)ly * F.res_x + px);
         return sky;
     }
     if (active2 && s == 0) {
@@ -560,26 +570,7 @@ __device__ __forceinline__ bool render_sample_wave(const SceneDev &S, const Fram
         cnt.shadow += n_sh;
         cnt.reflection += n_rf;
         cnt.moot += n_mo;
-        // render_tile's hand-off, for the sample of lane `part`
-        typedef __attribute__((address_space(1))) unsigned gu32;
-        typedef __attribute__((address_space(1))) int gi32;
-        float *sp = F.split_samples + ((size_t)sidx * kWaveSize + part) * 4;
-        __hip_atomic_store((gu32 *)sp, __float_as_uint(color.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu32 *)(sp + 1), __float_as_uint(color.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((gu32 *)(sp + 2), __float_as_uint(color.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int *cp = F.split_count + sidx * (kWaveSize / 4) + (part >> 2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sample is visible before the count
-        if (__hip_atomic_fetch_add((gi32 *)cp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
-            const float *b = F.split_samples + ((size_t)sidx * kWaveSize + (part & ~3)) * 4;
-            auto ld = [](const float *q) {
-                return __uint_as_float(__hip_atomic_load((gu32 *)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            };
-            f3 v = mk(ld(b), ld(b + 1), ld(b + 2));
-            for (int k = 1; k < 4; ++k) v = v + mk(ld(b + 4 * k), ld(b + 4 * k + 1), ld(b + 4 * k + 2));
-            v = v * 0.25f;
-            rts::store_pixel(F, (size_t)ly * F.res_x + px, v);
-            __hip_atomic_store((gi32 *)cp, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
-        }
+        split_handoff(F, sidx, part, color, (size_t)ly * F.res_x + px);  // render_tile's, for lane `part`'s sample
     }
     return sky;
 }
