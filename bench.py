@@ -152,6 +152,39 @@ def roofline(pmc, pmc_state, kernel_name, avg_kernel_s, logical):
     return out
 
 
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate over the 8 XCDs
+
+
+def fetched_leg(config, avg_kernel_s, rt, fr, whole_frame):
+    """The memory side a packet tracer has: the bytes a
+    frame's traversal and shading request from the cache hierarchy — scalar
+    packet fetches once per wave, per-lane fetches once per lane — counted by
+    the RT_FETCH_COUNT measuring build (tools/fetch_bytes.py) and pinned in
+    profiles/canonical_counts.json; re-measured here with that build when it
+    is present (`state`: match / mismatch), priced against the L2's
+    bandwidth.  Whole frames only."""
+    if not whole_frame:
+        return {"state": "n/a (row band)"}
+    p = os.path.join(ROOT, "profiles", "canonical_counts.json")
+    e = json.load(open(p)).get(config, {}) if os.path.exists(p) else {}
+    committed = e.get("fetched_bytes_per_frame")
+    live = None
+    variant = os.path.join(ROOT, "unity-raytracer_amd", "lib", "variants", "fetch", "librt_mi355.so")
+    if os.path.exists(variant):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from fetch_bytes import timed_path_fetch  # noqa: E402
+        live, _, _ = timed_path_fetch(rt, fr, lib_path=variant)
+    b = live if live is not None else committed
+    if b is None:
+        return {"state": "missing"}
+    a = b / avg_kernel_s / 1e9
+    return {"bytes_per_launch": b, "achieved": a, "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": a / L2_PEAK_GBS,
+            "committed_bytes_per_launch": committed,
+            "state": ("match" if live is not None and committed is not None and abs(live - committed) <= 1e-6 * committed
+                      else "mismatch" if live is not None and committed is not None
+                      else "live (not committed)" if live is not None else "committed (no measuring build)")}
+
+
 def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     """The trace kernel instance a frame launches (rtk::launch_render_mega and
     lpt_prepare in csrc/trace.hip / csrc/rt_frame.cpp): the all-packet levels
@@ -764,6 +797,8 @@ def main():
             kname = timed_launch.split()[0]
             pmc, pmc_state = None, f"not measured for batch launches ({batch} frames a launch)"
         rays_per_frame = rays // args.steps
+        fetched = fetched_leg(args.config, avg_kernel_s, rt, fr,
+                              band_count == 1 and batch == 1 and args.mode == "megakernel")
         line = {
             "metric": METRIC,
             "value": rays / elapsed / 1e6,
@@ -817,6 +852,8 @@ def main():
                 "host_enqueue_ms_per_frame": host_s / args.steps * 1e3,
             },
             "roofline": {**roofline(pmc, pmc_state, kname, avg_kernel_s, logical), "canonical_counts": canonical,
+                         # the requested (cache-level) bytes: per-wave packet fetches, per-lane chain fetches
+                         "fetched_bytes_per_launch": fetched.get("bytes_per_launch"), "fetched": fetched,
                          # whole frames in flight: the order's sky tail in a second launch per frame
                          # (trace.hip sky_batch_kernel); avg_kernel_ms and the counters cover both
                          **({"with": "sky_batch_batch_kernel" if batch > 1 else
