@@ -20,6 +20,7 @@ a cpu_baseline measured with the C oracle (single-thread brute force, the
 reference's algorithm) on a bounded pixel sample of the same frame.
 """
 import argparse
+import collections
 import hashlib
 import json
 import os
@@ -396,6 +397,9 @@ def main():
                     help="frames per launch (rt_render_device_batch: frames of one layout from their own cameras as "
                          "one launch, their tiles under one longest-first order); 0 = 8 for a rank's row band "
                          "(N > 1 or --sim-bands: each band alone is too small to fill the GPU), 1 otherwise")
+    ap.add_argument("--pace", type=int, default=1,
+                    help="whole frames on one GPU: each frame to the stream with the fewest unfinished frames (at "
+                         "most 2 a stream; 0 = round robin)")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--sim-bands", type=int, default=0,
                     help="experiment (one GPU, no gather): render only row band 0 of N, i.e. one rank's share "
@@ -565,6 +569,31 @@ def main():
 
     batch_cams = []
     batch_no = [0]
+    # The frame queue of whole frames on one GPU (--pace): the next frame goes
+    # to the stream with the fewest unfinished frames, at most PACE_DEPTH per
+    # stream (the host waits for a slot, as a renderer waits for a free
+    # swap-chain image).  Round robin gave every stream the same number of
+    # frames although the hardware serves its queues unevenly: in a 20-frame
+    # window two streams ended 1.3 ms before the others (r07g kernel trace).
+    pace = args.pace and not dist_on and batch == 1 and nstreams > 1 and nbuf == nstreams
+    PACE_DEPTH = 2
+    pending = [collections.deque() for _ in range(nstreams)]
+
+    pace_wait = [0.0]  # host seconds spent waiting for a slot (not enqueue work)
+
+    def pick_stream():
+        tw = None
+        while True:
+            for q in pending:
+                while q and q[0].query():
+                    q.popleft()
+            i = min(range(nstreams), key=lambda k: len(pending[k]))
+            if len(pending[i]) < PACE_DEPTH:
+                if tw is not None:
+                    pace_wait[0] += time.perf_counter() - tw
+                return i
+            if tw is None:
+                tw = time.perf_counter()
 
     def flush_batch():
         """The pending frames of the current group as one launch on the
@@ -596,6 +625,8 @@ def main():
         f = frame_no[0]
         b = f % nbuf
         g, j = b // G, b % G
+        if pace:
+            b = pick_stream()  # (one output buffer per stream: nbuf == nstreams here)
         sb = streams[(j if dist_on else b) % nstreams]
         last_frame[0] = f
         ctx.set_stream(sb.cuda_stream)
@@ -607,6 +638,10 @@ def main():
             else:
                 sb.wait_event(freed[g])
         ctx.render_device(cam or cam_s, plane_s, aparams, outs[b].data_ptr(), nbytes)
+        if pace:
+            ev = torch.cuda.Event()  # (a fresh one: a slow stream's pending event may be any age)
+            ev.record(sb)
+            pending[b].append(ev)
         if dist_on and j == G - 1:
             close_group(g, G)
         frame_no[0] += 1
@@ -668,9 +703,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    pace_wait[0] = 0.0
     for _ in range(args.steps):
         step()
-    host_s = time.perf_counter() - t0  # host time to enqueue the K frames
+    host_s = time.perf_counter() - t0 - pace_wait[0]  # host time to enqueue the K frames (not the slot waits)
     drain()
     st = ctx.finish()
     ctx.set_stream(stream.cuda_stream)
@@ -833,6 +869,8 @@ def main():
                 "shadow_rays_moot": moot // args.steps,
                 "mrays_per_s_traversed": (rays - moot) / elapsed / 1e6,
                 "frames_in_flight": batch * min(ngroups, nstreams) if batch > 1 else nstreams,
+                "frame_queue": f"paced: <= {PACE_DEPTH} unfinished frames a stream, the next to the emptiest" if pace
+                else "round robin",
                 "timed_launch": timed_launch,
                 "lone_launch": lone_launch,
                 "frames_per_gather": G if dist_on else None,

@@ -590,6 +590,47 @@ def test_one_sample_waves_trace_with_the_whole_wave(gpu_ctx, rt, name, cap):
         assert lib.rt_debug_set(gpu_ctx.h, rt.abi.RT_DEBUG_SAMPLE_WAVE_STACK, 0) == 0
 
 
+def test_one_sample_handoff_under_concurrent_streams(rt):
+    """The one-sample waves' relaxed hand-off (trace.hip split_handoff: the
+    samples by agent-scope stores, a wait, a relaxed count, the last arrival's
+    agent-scope loads) with other work on the GPU: four contexts, each on its
+    own stream, render lone 1/8 shares of C3 concurrently (each frame is lone
+    in its context, so it runs one-sample waves: s16_shift=0), frame after
+    frame; every pixel of every frame equals the unsplit row-major share."""
+    import torch
+    fr = rt.make("C3")
+    ctxs, streams, outs, refs = [], [], [], []
+    try:
+        for k in range(4):
+            c = rt.Context()
+            c.set_scene(fr.scene)
+            kw = dict(band_index=2 * k + 1, band_count=8, band_rows=8)
+            ref, _ = c.render(fr.camera, fr.plane, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ROW_ORDER, **kw))
+            s = torch.cuda.Stream()
+            c.set_stream(s.cuda_stream)
+            ctxs.append((c, rt.frame_params(fr, flags=rt.abi.RT_FLAG_ASYNC, **kw)))
+            streams.append(s)
+            outs.append(torch.empty(ref.shape, dtype=torch.float32, device="cuda"))
+            refs.append(ref)
+        for f in range(8):
+            for k, (c, p) in enumerate(ctxs):
+                outs[k].fill_(float("nan"))
+            torch.cuda.synchronize()
+            for k, (c, p) in enumerate(ctxs):  # enqueued back to back: the four run at once
+                c.render_device(fr.camera, fr.plane, p, outs[k].data_ptr(), outs[k].numel() * 4)
+            for k, (c, p) in enumerate(ctxs):
+                c.finish()
+            torch.cuda.synchronize()
+            for k, (c, p) in enumerate(ctxs):
+                if f >= 2:  # from the third frame on the order exists and the slowest pixels run as one-sample waves
+                    assert "s16_shift=0" in c.last_launch(), c.last_launch()
+                assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), refs[k].view(np.uint32)), (f, k)
+    finally:
+        for c, _ in ctxs:
+            c.set_stream(None)
+            c.close()
+
+
 def test_split_sixteenths_of_large_shards_is_invisible(gpu_ctx, rt):
     """Shards of 24,000-70,000 tiles (a 1/2 and a 1/4 shard of 1080p C3) run
     their slowest tiles finely split — synchronous (lone) frames their slowest

@@ -359,18 +359,22 @@ constexpr int kMkThreads = kMkWaves * kWaveSize;
 // The hand-off of a one-sample wave's sample (a lone shard's finely split
 // pixel, F.s16_shift 0): the sample goes to the pixel's slots, then the
 // pixel's arrival count; the fourth arrival sums the four samples in sample
-// order (as sample_sum) and stores the pixel.  Two forms (A/B: RT_EXP_RELAXED):
-// * release / acquire (the default since round 6): a release fetch-add of the
-//   count and an acquire fence in the last arrival — the C++ memory model's
-//   hand-off, at agent scope (the arrivals run on any XCD);
-// * relaxed (round 5): the samples as agent-scope (write-through) stores, an
-//   explicit wait for them before a relaxed count, agent-scope loads after it
-//   — the same hand-off on gfx950 without the L2 write-back an agent-scope
-//   release costs, but argued from the ISA rather than the memory model.
-#ifdef RT_EXP_RELAXED
-constexpr bool kRelAcqHandoff = false;  // measuring builds only
+// order (as sample_sum) and stores the pixel.  Two forms (A/B: RT_EXP_RELACQ):
+// * relaxed (the default): the samples as agent-scope (write-through) stores,
+//   an explicit wait for them before a relaxed count, agent-scope loads after
+//   it — the hand-off a release / acquire pair gives, on gfx950, without the
+//   L2 write-back an agent-scope release costs; argued from the ISA (the
+//   samples reach the device's coherence point before the count; the last
+//   arrival reads that point, after its count returned), and checked by
+//   tests/test_gpu_parity.py::test_one_sample_handoff_under_concurrent_streams;
+// * release / acquire: a release fetch-add of the count and an acquire fence
+//   in the last arrival — the C++ memory model's hand-off at agent scope.  A
+//   lone 1/8 C3 share 0.100 -> 0.143 ms (+42 %, three alternating rounds,
+//   r07g): each release writes back the L2.
+#ifdef RT_EXP_RELACQ
+constexpr bool kRelAcqHandoff = true;  // measuring builds only
 #else
-constexpr bool kRelAcqHandoff = true;
+constexpr bool kRelAcqHandoff = false;
 #endif
 __device__ __forceinline__ void split_handoff(const FrameDev &F, int sidx, int slot, f3 color, size_t pixel) {
     typedef __attribute__((address_space(1))) unsigned gu32;
