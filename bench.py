@@ -577,18 +577,17 @@ def main():
     # window two streams ended 1.3 ms before the others (r07g kernel trace).
     pace = args.pace and not dist_on and batch == 1 and nstreams > 1 and nbuf == nstreams
     PACE_DEPTH = 2
-    pending = [collections.deque() for _ in range(nstreams)]
-
+    pace_q = [collections.deque() for _ in range(nstreams)]  # per stream: events of its unfinished frames
     pace_wait = [0.0]  # host seconds spent waiting for a slot (not enqueue work)
 
     def pick_stream():
         tw = None
         while True:
-            for q in pending:
+            for q in pace_q:
                 while q and q[0].query():
                     q.popleft()
-            i = min(range(nstreams), key=lambda k: len(pending[k]))
-            if len(pending[i]) < PACE_DEPTH:
+            i = min(range(nstreams), key=lambda k: len(pace_q[k]))
+            if len(pace_q[i]) < PACE_DEPTH:
                 if tw is not None:
                     pace_wait[0] += time.perf_counter() - tw
                 return i
@@ -641,7 +640,7 @@ def main():
         if pace:
             ev = torch.cuda.Event()  # (a fresh one: a slow stream's pending event may be any age)
             ev.record(sb)
-            pending[b].append(ev)
+            pace_q[b].append(ev)
         if dist_on and j == G - 1:
             close_group(g, G)
         frame_no[0] += 1
