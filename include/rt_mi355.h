@@ -371,9 +371,10 @@ int rt_update_mesh_transforms(rt_ctx *ctx, const float *local_to_world, int32_t 
  * the top row, alpha = 1), i.e. PixelColors.  When band_count > 1, only this
  * shard's rows are rendered and out_rgba receives the shard's compact
  * buffer (rt_band_rows_local rows); on a multi-device context such a frame
- * runs on device 0 only.  The device-to-host copy is overlapped with the
- * rendering: the frame is rendered in row slabs (alternating over two
- * streams) and each finished slab is copied while later slabs render. */
+ * runs on device 0 only.  Copy-bound formats (float RGBA frames of 2 MB or
+ * more) overlap the device-to-host copy with the rendering: row slabs
+ * alternating over two streams, each finished slab copied while later slabs
+ * render; other frames render in one piece with the copy right behind. */
 int rt_render(rt_ctx *ctx, const rt_camera *camera, const rt_image_plane *plane,
               const rt_render_params *params, void *out_rgba, rt_stats *stats);
 
@@ -412,7 +413,10 @@ int rt_render_device_batch(rt_ctx *ctx, int32_t num_frames, const rt_camera *cam
                            size_t frame_stride_bytes, rt_stats *stats);
 
 /* Rows of the compact per-shard buffer for (resolution_y, band_index,
- * band_count, band_rows). */
+ * band_count, band_rows): the same for every shard, so the last shards of a
+ * ragged split end in padding rows (blocks past the image).  Padding rows
+ * are not part of the image: no render writes them (rt_render's host buffer
+ * may hold whatever the device buffer held) and rt_assemble_bands skips them. */
 int32_t rt_band_rows_local(int32_t resolution_y, int32_t band_index, int32_t band_count,
                            int32_t band_rows);
 
