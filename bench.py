@@ -397,9 +397,9 @@ def main():
                     help="frames per launch (rt_render_device_batch: frames of one layout from their own cameras as "
                          "one launch, their tiles under one longest-first order); 0 = 8 for a rank's row band "
                          "(N > 1 or --sim-bands: each band alone is too small to fill the GPU), 1 otherwise")
-    ap.add_argument("--pace", type=int, default=1,
-                    help="whole frames on one GPU: each frame to the stream with the fewest unfinished frames (at "
-                         "most 2 a stream; 0 = round robin)")
+    ap.add_argument("--pace", type=int, default=2,
+                    help="whole frames on one GPU: each frame to the stream with the fewest unfinished frames, at "
+                         "most this many a stream (0 = round robin)")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--sim-bands", type=int, default=0,
                     help="experiment (one GPU, no gather): render only row band 0 of N, i.e. one rank's share "
@@ -575,8 +575,8 @@ def main():
     # swap-chain image).  Round robin gave every stream the same number of
     # frames although the hardware serves its queues unevenly: in a 20-frame
     # window two streams ended 1.3 ms before the others (r07g kernel trace).
-    pace = args.pace and not dist_on and batch == 1 and nstreams > 1 and nbuf == nstreams
-    PACE_DEPTH = 2
+    pace = args.pace > 0 and not dist_on and batch == 1 and nstreams > 1 and nbuf == nstreams
+    PACE_DEPTH = args.pace
     pace_q = [collections.deque() for _ in range(nstreams)]  # per stream: events of its unfinished frames
     pace_wait = [0.0]  # host seconds spent waiting for a slot (not enqueue work)
 
