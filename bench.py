@@ -37,8 +37,13 @@ sys.path.insert(0, ROOT)
 # default of 4 queues per process serialises a fourth render stream behind
 # another (measured on a 1/8 shard: 4 streams 13.7 Grays/s per rank with 4
 # queues, 22.7 with 8).  Set before the HIP runtime initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# (--hw-queues N, read here before argparse: experiments with more streams; at most 32 on this pool)
+_hwq = 8
+for _i, _a in enumerate(sys.argv[:-1]):
+    if _a == "--hw-queues":
+        _hwq = max(1, min(32, int(sys.argv[_i + 1])))
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < _hwq:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_hwq)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402  (import before the HIP library: one HIP runtime)
@@ -400,6 +405,8 @@ def main():
     ap.add_argument("--pace", type=int, default=2,
                     help="whole frames on one GPU: each frame to the stream with the fewest unfinished frames, at "
                          "most this many a stream (0 = round robin)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="hardware queues per process (GPU_MAX_HW_QUEUES, raised to this before HIP starts)")
     ap.add_argument("--lib", default="", help="experiment: library variant under unity-raytracer_amd/lib/variants/")
     ap.add_argument("--sim-bands", type=int, default=0,
                     help="experiment (one GPU, no gather): render only row band 0 of N, i.e. one rank's share "
