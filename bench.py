@@ -201,7 +201,7 @@ def trace_kernel_name(mode, spp, depth, res_x, local_rows, in_flight=True):
     overlapped_frame; `in_flight` False: frames one at a time) — Q4 for 2x2
     spp, W the waves per SIMD (5 for shards of <= 70,000 tiles and deep
     frames, else 6), SAMPLE (the sixth) for the lone-shard instance whose
-    one-sample waves trace with the whole wave (csrc/coop.h).  The bench's timed frames are in flight (four streams):
+    one-sample waves trace with the whole wave (csrc/coop.h).  The bench's timed frames are in flight (eight streams):
     whole frames run the non-split instance."""
     if mode == "packet":
         return "render_packet_kernel<false, true>"
@@ -393,16 +393,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: check the assembled frame against 1 rank")
     ap.add_argument("--mode", choices=["megakernel", "wavefront", "packet"], default="megakernel")
-    ap.add_argument("--streams", type=int, default=4,
-                    help="HIP streams consecutive frames alternate on: frames in flight, so one frame's slowest "
-                         "tiles overlap the next frame's bulk (1 = one frame at a time)")
+    ap.add_argument("--streams", type=int, default=8,
+                    help="HIP streams the frames are queued on: frames in flight, so one frame's slowest tiles "
+                         "overlap the next frames' bulk (1 = one frame at a time; 8 since r07n: the driver's "
+                         "command 54.7 Grays/s against 51.8 with 4 streams two deep)")
     ap.add_argument("--gather-frames", type=int, default=0,
                     help="N > 1: frames per RCCL gather (one collective per group of frames; 0 = --streams)")
     ap.add_argument("--batch", type=int, default=0,
                     help="frames per launch (rt_render_device_batch: frames of one layout from their own cameras as "
                          "one launch, their tiles under one longest-first order); 0 = 8 for a rank's row band "
                          "(N > 1 or --sim-bands: each band alone is too small to fill the GPU), 1 otherwise")
-    ap.add_argument("--pace", type=int, default=2,
+    ap.add_argument("--pace", type=int, default=1,
                     help="whole frames on one GPU: each frame to the stream with the fewest unfinished frames, at "
                          "most this many a stream (0 = round robin)")
     ap.add_argument("--hw-queues", type=int, default=8,
@@ -582,6 +583,12 @@ def main():
     # swap-chain image).  Round robin gave every stream the same number of
     # frames although the hardware serves its queues unevenly: in a 20-frame
     # window two streams ended 1.3 ms before the others (r07g kernel trace).
+    # Default: eight streams one deep — every queued frame runs, none waits
+    # behind another on its stream, so a window's last frames drain together
+    # (alternating lines, r07i/r07l/r07m/r07n: the driver's command 49.7 with
+    # four streams in rotation, 51.8 four streams two deep, 54.0 four one
+    # deep, 54.7 eight one deep; 200 frames 53.3 / 58.2 / 57.5 / 59.4; eight
+    # streams two deep 52.6 / 59.3, twelve 50.9 / 57.8)
     pace = args.pace > 0 and not dist_on and batch == 1 and nstreams > 1 and nbuf == nstreams
     PACE_DEPTH = args.pace
     pace_q = [collections.deque() for _ in range(nstreams)]  # per stream: events of its unfinished frames

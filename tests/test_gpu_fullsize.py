@@ -1,7 +1,8 @@
 """Full-size, whole-frame parity of the exact paths the bench times
 (VERDICT r04 "Next" item 2; SURVEY §8(a) rows A1-A14 at BASELINE sizes).
 
-* The timed path: bench.py's loop — a fresh context, four HIP streams,
+* The timed path: bench.py's loop — a fresh context, eight HIP streams one
+  frame deep (each frame to a stream whose previous frame has ended),
   RT_FLAG_ASYNC frames into device buffers (rt_render_device), enough frames
   that longest-first dispatch runs from a measured order and every stream
   has a frame beside it, so the frames run the in-flight instance
@@ -19,7 +20,7 @@
 * C4 (3840x2160, 16 spp) and C5 (250k triangles, 64 spp, depth 16) whole
   frames (render_levels_kernel): every 16th row against the tree walk, plus
   brute force on seeded pixels.
-* C4's timed path (bench.py --config C4): four streams of RT_FLAG_ASYNC
+* C4's timed path (bench.py --config C4): eight streams of RT_FLAG_ASYNC
   frames, the levels kernel in flight with its 16-spp sky batches (the
   measured non-sky tiles as stripes, the sky tail in sky_batch_kernel), every
   16th row of every stream's frame against the tree walk, ray counts against
@@ -83,7 +84,7 @@ def test_timed_path_full_frame_equals_oracle(rt, orc, name):
     fr = rt.make(name)
     W, H = fr.plane.ResolutionX, fr.plane.ResolutionY
     ctx = rt.Context()
-    streams = [torch.cuda.Stream() for _ in range(4)]
+    streams = [torch.cuda.Stream() for _ in range(8)]
     try:
         ctx.set_stream(streams[0].cuda_stream)
         ctx.set_scene(fr.scene)
@@ -97,11 +98,19 @@ def test_timed_path_full_frame_equals_oracle(rt, orc, name):
             ctx.render_device(cam, pl, p, outs[k].data_ptr(), nbytes)
         ctx.finish()
         torch.cuda.synchronize()
-        frames, launches = 36, []
-        for f in range(frames):  # nine per stream, each stream's order measured by its setup frame
-            k = f % len(streams)
+        frames, launches, used = 48, [], [0] * len(streams)
+        done = [None] * len(streams)  # per stream: the event of its unfinished frame (bench.py's paced queue)
+        for f in range(frames):
+            while True:  # a stream whose previous frame has ended (each stream's order measured by its setup frame)
+                free = [k for k in range(len(streams)) if done[k] is None or done[k].query()]
+                if free:
+                    break
+            k = min(free, key=lambda j: used[j])
+            used[k] += 1
             ctx.set_stream(streams[k].cuda_stream)
             ctx.render_device(cam, pl, p, outs[k].data_ptr(), nbytes)
+            done[k] = torch.cuda.Event()
+            done[k].record(streams[k])
             launches.append(ctx.last_launch())
         st = ctx.finish()
         torch.cuda.synchronize()
@@ -174,7 +183,7 @@ def test_c4_timed_path_in_flight_every_16th_row(rt, orc):
     fr = rt.make("C4")
     W, H = fr.plane.ResolutionX, fr.plane.ResolutionY
     ctx = rt.Context()
-    streams = [torch.cuda.Stream() for _ in range(4)]
+    streams = [torch.cuda.Stream() for _ in range(8)]  # bench.py's eight streams (one frame each here)
     try:
         ctx.set_stream(streams[0].cuda_stream)
         ctx.set_scene(fr.scene)

@@ -18,14 +18,14 @@ if [ "$bands" -gt 1 ]; then sfx=${cfg}_b$bands; band_arg="--band 0/$bands --rgb3
 kernel=$(python3 -c "import sys; sys.path.insert(0, '$R'); import bench, _rt_pkg; rt = _rt_pkg.load(); fr = rt.make('$cfg'); \
 rows = fr.plane.ResolutionY if $bands == 1 else -(-fr.plane.ResolutionY // (8 * $bands)) * 8; \
 print(bench.trace_kernel_name('megakernel', fr.spp, fr.max_bounces, fr.plane.ResolutionX, rows, in_flight=True))") || exit 1
-# the timed frames are RT_FLAG_ASYNC on four streams like bench.py's (frames in flight: the same kernel
+# the timed frames are RT_FLAG_ASYNC on eight streams like bench.py's (frames in flight: the same kernel
 # instance as the bench line's — a whole frame's non-split one; the first of them, with no frame beside
 # it, runs the split instance and is not counted: the summary keeps the named kernel's dispatches)
-frames=17
+frames=24
 out=$R/gpurun_out/pmc_${tag}_$sfx${VARIANT:+_$VARIANT}
 run() {
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $2 --output-format csv -d $out/$1 -o run -- \
-    python3 $R/tools/probe.py --config $cfg --modes megakernel --frames $frames --variants ${VARIANT:-default} --async-frames --streams 4 \
+    python3 $R/tools/probe.py --config $cfg --modes megakernel --frames $frames --variants ${VARIANT:-default} --async-frames --streams 8 \
       $band_arg > $out/$1.log 2>&1
 }
 mkdir -p $out
