@@ -59,7 +59,7 @@ def test_bench_single_gpu_line():
 def test_bench_rccl_path_one_rank_partial_groups():
     # 7 timed frames in groups of 4 (one partial group); 3 warmup frames
     p = _run([sys.executable, "bench.py", "--steps", "7", "--warmup", "3", "--no-cpu-baseline", "--force-dist",
-              "--verify"], env_extra={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port())})
+              "--verify", "--gather-frames", "4"], env_extra={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port())})
     assert _verified(p.stderr), p.stderr[-3000:]
     d = _metric_line(p.stdout)
     assert d["config"]["frames_per_gather"] == 4 and "RCCL" in d["config"]["parallelism"]
