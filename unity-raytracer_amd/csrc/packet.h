@@ -35,6 +35,16 @@ constexpr int kWaveStack = rtd::kStackTotal + rtd::kCutMax;
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 
+// Box tests of a packet's internal node for every lane, retired or not (a
+// retired lane's keys come out +inf through a -inf culling distance): no
+// exec-mask branch around them.  RT_EXP_PKBRANCH=0 keeps the branch
+// (measuring builds).
+#ifdef RT_EXP_PKBRANCH
+constexpr bool kPkBranchless = RT_EXP_PKBRANCH != 0;
+#else
+constexpr bool kPkBranchless = true;
+#endif
+
 // Wave-wide sort key of one child (bits of a float >= 0): +inf bits when no
 // lane needs it, the representative lane's entry distance when it hits,
 // FLT_MAX bits when only other lanes do.
@@ -338,6 +348,7 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             __builtin_amdgcn_global_load_lds((const void *)(S.nodes4 + v), (__attribute__((address_space(3))) void *)pf_dump, 4, 0, 0);
     };
 #endif
+    const int rep0 = __ffsll((long long)live0) - 1;  // closest hit: a live lane, fixed for the whole walk
     // any-hit: the leaf that retires the most lanes (the next frame's hint)
     int best_leaf = 0, best_retired = 0;  // wave-uniform
     int skip = 0;                         // the hinted leaf, never visited again
@@ -381,8 +392,12 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
 #endif
         if (node >= 0) {
             RT_FETCH_WAVE(cnt, 128);
-            float k0 = INFINITY, k1 = INFINITY, k2 = INFINITY, k3 = INFINITY;
+            float k0, k1, k2, k3;
             const int4 ch = rtt::cload(&S.nodes4[node].child);
+            // a retired lane culls every child through its culling distance
+            // (tf = -inf < tn): the same +inf keys as skipping it, without an
+            // exec-mask branch around the box tests (kPkBranchless)
+            const float tc = kPkBranchless ? (L.live ? L.tcull : -INFINITY) : L.tcull;
             if (same_signs) {
                 // the near and far plane rows of each axis are fetched
                 // directly (scalar loads at per-wave offsets), then 3 FMA +
@@ -392,23 +407,24 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                 const float4 nx = rtt::cload(pl + ox), fx = rtt::cload(pl + (1 - ox));
                 const float4 ny = rtt::cload(pl + 2 + oy), fy = rtt::cload(pl + (3 - oy));
                 const float4 nz = rtt::cload(pl + 4 + oz), fz = rtt::cload(pl + (5 - oz));
-                if (L.live) {
-                    k0 = rtt::child_key_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, L.tcull);
-                    k1 = rtt::child_key_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, L.tcull);
-                    k2 = rtt::child_key_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, L.tcull);
-                    k3 = rtt::child_key_nf(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, L.tcull);
-                    if (COUNT) cnt.box += 4;
+                k0 = k1 = k2 = k3 = INFINITY;
+                if (kPkBranchless || L.live) {
+                    k0 = rtt::child_key_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tc);
+                    k1 = rtt::child_key_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tc);
+                    k2 = rtt::child_key_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tc);
+                    k3 = rtt::child_key_nf(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tc);
                 }
             } else {
                 const rtd::BvhNode4 nd = rtt::cload(S.nodes4 + node);
-                if (L.live) {
-                    k0 = rtt::child_key(nd.lox.x, nd.hix.x, nd.loy.x, nd.hiy.x, nd.loz.x, nd.hiz.x, r, L.tcull);
-                    k1 = rtt::child_key(nd.lox.y, nd.hix.y, nd.loy.y, nd.hiy.y, nd.loz.y, nd.hiz.y, r, L.tcull);
-                    k2 = rtt::child_key(nd.lox.z, nd.hix.z, nd.loy.z, nd.hiy.z, nd.loz.z, nd.hiz.z, r, L.tcull);
-                    k3 = rtt::child_key(nd.lox.w, nd.hix.w, nd.loy.w, nd.hiy.w, nd.loz.w, nd.hiz.w, r, L.tcull);
-                    if (COUNT) cnt.box += 4;
+                k0 = k1 = k2 = k3 = INFINITY;
+                if (kPkBranchless || L.live) {
+                    k0 = rtt::child_key(nd.lox.x, nd.hix.x, nd.loy.x, nd.hiy.x, nd.loz.x, nd.hiz.x, r, tc);
+                    k1 = rtt::child_key(nd.lox.y, nd.hix.y, nd.loy.y, nd.hiy.y, nd.loz.y, nd.hiz.y, r, tc);
+                    k2 = rtt::child_key(nd.lox.z, nd.hix.z, nd.loy.z, nd.hiy.z, nd.loz.z, nd.hiz.z, r, tc);
+                    k3 = rtt::child_key(nd.lox.w, nd.hix.w, nd.loy.w, nd.hiy.w, nd.loz.w, nd.hiz.w, r, tc);
                 }
             }
+            if (COUNT && L.live) cnt.box += 4;
             if (ANY) {
                 // any-hit (shadow rays): the order cannot change the answer,
                 // so the children any live lane needs are taken in slot order
@@ -438,8 +454,8 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             // only affects speed.  Keys are >= 0, so their bit patterns order
             // as unsigned integers and the whole ordering runs on the scalar
             // unit.
-            const unsigned long long live_m = __ballot(L.live);
-            const int rep = __ffsll((long long)live_m) - 1;
+            // (a closest-hit packet's lanes never retire: its representative is fixed)
+            const int rep = rep0;
             unsigned q0 = wave_key_bits(k0, rep), q1 = wave_key_bits(k1, rep), q2 = wave_key_bits(k2, rep),
                      q3 = wave_key_bits(k3, rep);
             int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
