@@ -37,8 +37,11 @@ __device__ __forceinline__ float unif(float v) { return __int_as_float(__builtin
 
 // Box tests of a packet's internal node for every lane, retired or not (a
 // retired lane's keys come out +inf through a -inf culling distance): no
-// exec-mask branch around them.  RT_EXP_PKBRANCH=0 keeps the branch
-// (measuring builds).
+// exec-mask branch around them (packet_trace's BL).  The megakernel's
+// default (C3 +0.75 %, r07q); the levels kernel keeps the branch — without
+// it its register allocation spilled more (16-spp instance 6 -> 16 VGPR
+// spill slots; C5's scratch writes 1.91 -> 3.37 GB a frame, r07r).
+// RT_EXP_PKBRANCH=0: the megakernel with the branch (measuring builds).
 #ifdef RT_EXP_PKBRANCH
 constexpr bool kPkBranchless = RT_EXP_PKBRANCH != 0;
 #else
@@ -264,7 +267,7 @@ __device__ __forceinline__ CutStart cut_select(const rtd::SceneDev &S, const rtd
 // compiled only into the split-tile instance of render_kernel (small shards
 // and synchronous frames, whose time is their slowest waves: a 1/8 C3 shard
 // -3 %); in the whole-frame instance the extra scalar state cost 4 % (r04a).
-template <bool ANY, bool COUNT, bool HINT = false>
+template <bool ANY, bool COUNT, bool HINT = false, bool BL = kPkBranchless>
 __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCtx &r, bool part, float tlimit,
                                              float d2, PacketLane &L, int *wstack, Counts &cnt,
                                              const CutStart *cs = nullptr, int hint = 0, int *hint_out = nullptr) {
@@ -396,8 +399,8 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             const int4 ch = rtt::cload(&S.nodes4[node].child);
             // a retired lane culls every child through its culling distance
             // (tf = -inf < tn): the same +inf keys as skipping it, without an
-            // exec-mask branch around the box tests (kPkBranchless)
-            const float tc = kPkBranchless ? (L.live ? L.tcull : -INFINITY) : L.tcull;
+            // exec-mask branch around the box tests (BL)
+            const float tc = BL ? (L.live ? L.tcull : -INFINITY) : L.tcull;
             if (same_signs) {
                 // the near and far plane rows of each axis are fetched
                 // directly (scalar loads at per-wave offsets), then 3 FMA +
@@ -408,7 +411,7 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
                 const float4 ny = rtt::cload(pl + 2 + oy), fy = rtt::cload(pl + (3 - oy));
                 const float4 nz = rtt::cload(pl + 4 + oz), fz = rtt::cload(pl + (5 - oz));
                 k0 = k1 = k2 = k3 = INFINITY;
-                if (kPkBranchless || L.live) {
+                if (BL || L.live) {
                     k0 = rtt::child_key_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tc);
                     k1 = rtt::child_key_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tc);
                     k2 = rtt::child_key_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tc);
@@ -417,7 +420,7 @@ __device__ __forceinline__ void packet_trace(const rtd::SceneDev &S, const RayCt
             } else {
                 const rtd::BvhNode4 nd = rtt::cload(S.nodes4 + node);
                 k0 = k1 = k2 = k3 = INFINITY;
-                if (kPkBranchless || L.live) {
+                if (BL || L.live) {
                     k0 = rtt::child_key(nd.lox.x, nd.hix.x, nd.loy.x, nd.hiy.x, nd.loz.x, nd.hiz.x, r, tc);
                     k1 = rtt::child_key(nd.lox.y, nd.hix.y, nd.loy.y, nd.hiy.y, nd.loz.y, nd.hiz.y, r, tc);
                     k2 = rtt::child_key(nd.lox.z, nd.hix.z, nd.loy.z, nd.hiy.z, nd.loz.z, nd.hiz.z, r, tc);

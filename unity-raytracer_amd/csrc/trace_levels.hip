@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
         rtt::setup_ray(r, o, d);
         rtp::PacketLane P;
         RT_LSEG(const unsigned long long tp0 = __builtin_amdgcn_s_memtime();)
-        rtp::packet_trace<false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt,
+        rtp::packet_trace<false, false, false, false>(S, r, alive, 0.0f, 0.0f, P, wstack_mem, cnt,
                                         CUT && level == 0 ? &cs : nullptr);
         RT_LSEG(const unsigned long long tp = __builtin_amdgcn_s_memtime() - tp0;
                 if (level == 0) sg_cam += tp;
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
                                      sf.p.x, sf.p.y, sf.p.z, sf.n.x, sf.n.y, sf.n.z, sf.view.x, sf.view.y, sf.view.z};
 #pragma unroll
                 for (int i = 0; i < STASH; ++i) vs[i * kWaveSize] = v[i];
-                rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+                rtp::packet_trace<true, false, false, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
                 vs = stash_mem + rtt::lane_id();
                 col = mk(vs[0], vs[64], vs[128]);
                 lit = mk(vs[192], vs[256], vs[320]);
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kWaveSize, MIN_WAVES) void render_levels_kernel(Sce
                 }
                 if (STASH >= 18) sf.view = mk(vs[960], vs[1024], vs[1088]);
             } else {
-                rtp::packet_trace<true, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
+                rtp::packet_trace<true, false, false, false>(S, rs, trace, sqrtf(sr.d2) * 1.001f, sr.d2, Q, wstack_mem, cnt);
             }
             RT_LSEG(sg_sh += __builtin_amdgcn_s_memtime() - tq0;)
             if (trace && Q.best_rank != 1) col = lit;
