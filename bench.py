@@ -81,7 +81,7 @@ def canonical_check(config, st, whole_frame):
     if not os.path.exists(p):
         return {"state": "missing"}
     e = json.load(open(p)).get(config)
-    if not e:
+    if not e or "counts" not in e:  # (C4: only its fetched bytes are pinned — no oracle walk of a 4K frame)
         return {"state": "missing"}
     keys = ("primary_rays", "shadow_rays", "reflection_rays", "box_tests", "triangle_tests", "sphere_tests",
             "shading_fetches")

@@ -77,3 +77,21 @@ def test_bench_rejects_world_size_mismatch():
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--launch-check"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and "WORLD_SIZE 2" in p.stderr
+
+
+def test_bench_canonical_check_without_counts():
+    """profiles/canonical_counts.json pins only fetched bytes for C4 (no
+    oracle walk of a 4K frame): bench.py --config C4 reports the canonical
+    counts as missing instead of failing (r07s)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class St:
+        primary_rays = shadow_rays = reflection_rays = box_tests = triangle_tests = sphere_tests = 0
+        shading_fetches = 0
+
+    entries = json.load(open(os.path.join(ROOT, "profiles", "canonical_counts.json")))
+    assert "C4" in entries and "counts" not in entries["C4"]
+    assert bench.canonical_check("C4", St(), True) == {"state": "missing"}
+    assert bench.canonical_check("C3", St(), True)["state"] == "mismatch"
+    assert bench.canonical_check("C3", St(), False)["state"] == "n/a (row band)"
