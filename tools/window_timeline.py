@@ -25,6 +25,7 @@ def main():
     ap.add_argument("trace_dir")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--kernel", default="render_kernel<false, false, false, true, 6, false>")
+    ap.add_argument("--lone", default="render_kernel<false, true, false, true, 6, false>")
     ap.add_argument("--low", type=int, default=2)
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True)
@@ -33,9 +34,27 @@ def main():
     rows = []
     for f in files:
         for r in csv.DictReader(open(f)):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+            grid = int(float(r.get("Grid_Size") or r.get("Grid_Size_X") or 0))
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], grid,
+                         (r.get("Stream_Id"), r.get("Queue_Id"))))
     rows.sort()
-    renders = [r for r in rows if a.kernel in r[2]]
+    sq = {(r[0], r[2]): r[4] for r in rows}
+    rows = [r[:3] for r in rows]
+    # the timed frames: the last --steps launches of the in-flight instance
+    # before bench.py's lone frames (the longest run of back-to-back
+    # --lone launches; rt_render's row slabs later run the in-flight
+    # instance again)
+    run, best, best_at = 0, 0, None
+    for i, r in enumerate(rows):
+        if a.lone in r[2]:
+            run += 1
+            if run > best:
+                best, best_at = run, i - run + 1
+        elif "render" in r[2]:
+            run = 0
+    if best_at is None:
+        raise SystemExit(f"no {a.lone} launches")
+    renders = [r for r in rows[:best_at] if a.kernel in r[2]]
     if len(renders) < a.steps:
         raise SystemExit(f"{len(renders)} dispatches of {a.kernel}")
     timed = renders[-a.steps:]
@@ -43,7 +62,7 @@ def main():
     last_render_end = max(e for _, e, _ in timed)
     # the kernels of the window: everything that starts inside it up to the
     # last timed frame's tail kernels (sky batches / tallies), before the next render instance
-    after = [r for r in rows if r[0] > timed[-1][0] and a.kernel not in r[2] and "render" in r[2]]
+    after = [r for r in rows if r[0] > timed[-1][0] and "render" in r[2]]
     stop = after[0][0] if after else float("inf")
     win = [r for r in rows if t0 <= r[0] < stop]
     t1 = max(e for _, e, _ in win)
@@ -78,6 +97,7 @@ def main():
         "last_render_to_end_ms": round((t1 - last_render_end) / 1e6, 4),
         "idle_ms": round(idle_t, 4),
         f"below_{a.low}_kernels_ms": round(low_t, 4),
+        "stream_queue": sorted({"%s->%s" % sq[(s0, n)] for s0, _, n in timed}),
         "frame_ms": [round((e - s) / 1e6, 4) for s, e, _ in timed],
         "start_offsets_ms": [round((s - t0) / 1e6, 4) for s in starts],
     }
